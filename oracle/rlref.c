@@ -1,0 +1,1181 @@
+/*
+ * rlref.c — CPU ORACLE (test infrastructure only; see rlref.h header for the
+ * parity status: "parity unpinned" — KAT- and table-fixture-pinned only).
+ *
+ * Plain C restatement of the reference hot path.  Every function cites the
+ * reference file:line it restates (paths relative to /root/reference).
+ * Build: -O2 -ffp-contract=off, no fast-math (NaN/inf semantics: SURVEY F7).
+ */
+#include "rlref.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+
+
+#define MIN_POSITIVE 2.2250738585072014e-308 /* f64::MIN_POSITIVE */
+#define QF_NAN  1u
+#define QF_PINF 2u
+#define QF_NINF 4u
+#define MAXS 2048
+#define MAXA 6
+
+/* ======================================================================== */
+/* ln(x): fdlibm e_log.c algorithm (public, Sun 1993).  The reference calls   */
+/* f64::ln (src/action_selection/upper_confidence_bound.rs:36,57), i.e. the   */
+/* platform libm.  The GPU needs a bit-identical ln on host and device, so the */
+/* oracle and the product both evaluate this exact operation sequence.       */
+/* ======================================================================== */
+typedef union { double d; uint64_t u; } dbits;
+
+double rlo_log(double x) {
+    static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                        two54 = 1.80143985094819840000e+16,
+                        Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                        Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                        Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                        Lg7 = 1.479819860511658591e-01;
+    double hfsq, f, s, z, R, w, t1, t2, dk;
+    int32_t k, hx, i, j;
+    uint32_t lx;
+    dbits b;
+    b.d = x;
+    hx = (int32_t)(b.u >> 32);
+    lx = (uint32_t)b.u;
+    k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | lx) == 0) return -INFINITY;
+        if (hx < 0) return NAN;
+        k -= 54;
+        x *= two54;
+        b.d = x;
+        hx = (int32_t)(b.u >> 32);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    i = (hx + 0x95f64) & 0x100000;
+    b.d = x;
+    b.u = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (b.u & 0xffffffffu);
+    x = b.d;
+    k += (i >> 20);
+    f = x - 1.0;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    s = f / (2.0 + f);
+    dk = (double)k;
+    z = s * s;
+    i = hx - 0x6147a;
+    w = z * z;
+    j = 0x6b851 - hx;
+    t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    R = t2 + t1;
+    if (i > 0) {
+        hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+/* ======================================================================== */
+/* RNG: the reference draws from rand::thread_rng() (ChaCha12, entropy       */
+/* seeded) at: frozen_lake.rs:156-157,175; taxi.rs:446-447; blackjack.rs:562 */
+/* (via :541); uniform_epsilon_greed.rs:51-54,62.  All sites share one        */
+/* thread-local stream.  Replacement: one xoshiro128** stream per lane,       */
+/* seeded by splitmix64(seed + lane*C); next_u64 = lo word then hi word.      */
+/* ======================================================================== */
+typedef struct { uint32_t s[4]; } rlo_rng;
+
+static uint64_t splitmix64(uint64_t *x) {
+    uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static void rng_seed(rlo_rng *r, uint64_t seed, uint64_t lane) {
+    uint64_t x = seed + lane * 0x632BE59BD9B4E019ull;
+    uint64_t a = splitmix64(&x), b = splitmix64(&x);
+    r->s[0] = (uint32_t)a; r->s[1] = (uint32_t)(a >> 32);
+    r->s[2] = (uint32_t)b; r->s[3] = (uint32_t)(b >> 32);
+    if ((r->s[0] | r->s[1] | r->s[2] | r->s[3]) == 0) r->s[0] = 1;
+}
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+static inline uint32_t next_u32(rlo_rng *r) {
+    uint32_t *s = r->s;
+    uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+    uint32_t t = s[1] << 9;
+    s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl32(s[3], 11);
+    return result;
+}
+static inline uint64_t next_u64(rlo_rng *r) {
+    uint64_t lo = next_u32(r);
+    uint64_t hi = next_u32(r);
+    return lo | (hi << 32);
+}
+void rlo_rng_stream(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out) {
+    rlo_rng r;
+    rng_seed(&r, seed, lane);
+    for (uint32_t i = 0; i < n; ++i) out[i] = next_u32(&r);
+}
+
+/* rand 0.8.5 UniformFloat<f64>::sample for Uniform::from(0.0..1.0):
+ * value1_2 = from_bits((u64 >> 12) | bits(1.0)); value0_1 = value1_2 - 1.0;
+ * result = value0_1 * scale(=1.0) + low(=0.0). */
+double rlo_u64_to_uniform01(uint64_t bits) {
+    dbits b;
+    b.u = (bits >> 12) | 0x3FF0000000000000ull;
+    double v = b.d - 1.0;
+    return v * 1.0 + 0.0;
+}
+static inline double uniform01(rlo_rng *r) { return rlo_u64_to_uniform01(next_u64(r)); }
+
+/* rand 0.8.5 UniformInt<usize>::sample (widening multiply + rejection zone),
+ * for Uniform::from(0..COUNT) (uniform_epsilon_greed.rs:34,62). */
+uint32_t rlo_uniform_int_u64(uint64_t v, uint64_t range, int *reject) {
+    uint64_t ints_to_reject = (UINT64_MAX - range + 1) % range;
+    uint64_t zone = UINT64_MAX - ints_to_reject;
+    unsigned __int128 m = (unsigned __int128)v * range;
+    uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+    *reject = !(lo <= zone);
+    return (uint32_t)hi;
+}
+static uint32_t uniform_action(rlo_rng *r, uint32_t A) {
+    for (;;) {
+        int rej;
+        uint32_t a = rlo_uniform_int_u64(next_u64(r), A, &rej);
+        if (!rej) return a;
+    }
+}
+/* rand 0.8.5 UniformInt<u8> (u32 large type) for Uniform::from(1..11)
+ * (blackjack.rs:542,562): range 10, ints_to_reject = (2^32-10)%10 = 6. */
+uint32_t rlo_uniform_card_u32(uint32_t v, int *reject) {
+    const uint32_t zone = 0xFFFFFFFFu - 6u;
+    uint64_t m = (uint64_t)v * 10u;
+    uint32_t hi = (uint32_t)(m >> 32), lo = (uint32_t)m;
+    *reject = !(lo <= zone);
+    return 1u + hi;
+}
+static uint32_t draw_card(rlo_rng *r) {
+    for (;;) {
+        int rej;
+        uint32_t c = rlo_uniform_card_u32(next_u32(r), &rej);
+        if (!rej) return c;
+    }
+}
+
+/* fxhash 0.2.1 FxHasher64 over #[derive(Hash)] BlackJackObservation
+ * (blackjack.rs:10-27): write_u8(p), write_u8(d), write_u8(ace as u8);
+ * h = (rotl(h,5) ^ byte) * 0x517cc1b727220a95, h0 = 0. */
+uint64_t rlo_blackjack_obs_id(uint32_t p, uint32_t d, uint32_t ace) {
+    const uint64_t K = 0x517cc1b727220a95ull;
+    uint64_t h = 0;
+    uint32_t w[3] = {p & 0xff, d & 0xff, ace ? 1u : 0u};
+    for (int i = 0; i < 3; ++i) h = (((h << 5) | (h >> 59)) ^ (uint64_t)w[i]) * K;
+    return h;
+}
+
+/* ======================================================================== */
+/* utils (src/utils.rs)                                                      */
+/* ======================================================================== */
+/* argmax: src/utils.rs:1-11 — first maximum, strict `>` */
+static inline uint32_t argmax_d(const double *v, uint32_t n) {
+    double m = v[0];
+    uint32_t res = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (v[i] > m) { m = v[i]; res = i; }
+    return res;
+}
+/* max: src/utils.rs:13-21 */
+static inline double max_d(const double *v, uint32_t n) {
+    double m = v[0];
+    for (uint32_t i = 0; i < n; ++i)
+        if (v[i] > m) m = v[i];
+    return m;
+}
+/* categorical_sample: src/utils.rs:33-43 — running sum, first b > u, else 0 */
+static uint32_t categorical_sample(const double *p, uint32_t n, double u) {
+    double b = 0.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        b += p[i];
+        if (b > u) return i;
+    }
+    return 0;
+}
+/* inc: src/utils.rs:53-76 — LEFT/DOWN/RIGHT/UP with clamping */
+static void inc(uint32_t nrow, uint32_t ncol, uint32_t row, uint32_t col, uint32_t a,
+                uint32_t *nr, uint32_t *nc) {
+    *nr = row; *nc = col;
+    if (a == 0) *nc = col != 0 ? col - 1 : 0;
+    else if (a == 1) *nr = row + 1 < nrow - 1 ? row + 1 : nrow - 1;
+    else if (a == 2) *nc = col + 1 < ncol - 1 ? col + 1 : ncol - 1;
+    else if (a == 3) *nr = row != 0 ? row - 1 : 0;
+}
+
+/* ======================================================================== */
+/* environments                                                              */
+/* ======================================================================== */
+typedef struct {
+    int kind;
+    uint32_t S, A, max_steps;
+    /* table envs: per (s,a) 3 outcomes */
+    double prob[MAXS * MAXA * 3];
+    uint32_t next[MAXS * MAXA * 3];
+    double rew[MAXS * MAXA * 3];
+    uint8_t term[MAXS * MAXA * 3];
+    double start[MAXS];
+    uint32_t n_start;
+    double trunc_reward;
+} envdef;
+
+typedef struct {
+    uint32_t pos, curr_step;
+    int ready;
+    uint32_t p_sum, d_sum, d0, p_ace, d_ace; /* blackjack */
+} envstate;
+
+static const char *FL4[4] = {"SFFF", "FHFH", "FFFH", "HFFG"};        /* frozen_lake.rs:23 */
+static const char *FL8[8] = {"SFFFFFFF", "FFFFFFFF", "FFFHFFFF", "FFFFFHFF",
+                             "FFFHFFFF", "FHHFFFHF", "FHFFHFHF", "FFFHFFFG"}; /* :25-28 */
+static const char *TAXI_MAP[7] = {"+---------+", "|R: | : :G|", "| : | : : |", "| : : : : |",
+                                  "| | : | : |", "|Y| : |B: |", "+---------+"}; /* taxi.rs:22-30 */
+static const uint32_t TAXI_LOCS[4][2] = {{0, 0}, {0, 4}, {4, 0}, {4, 3}};  /* taxi.rs:31 */
+
+static void set_outcome(envdef *E, uint32_t s, uint32_t a, int i, double p, uint32_t n, double r,
+                        int t) {
+    size_t k = ((size_t)s * E->A + a) * 3 + (size_t)i;
+    E->prob[k] = p; E->next[k] = n; E->rew[k] = r; E->term[k] = (uint8_t)t;
+}
+
+/* FrozenLakeEnv::new: src/env/frozen_lake.rs:48-102 */
+static void build_frozen_lake(envdef *E, int map8, int slippery) {
+    const char **map = map8 ? FL8 : FL4;
+    uint32_t n = map8 ? 8 : 4;
+    E->S = n * n; E->A = 4;
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < E->S; ++i) if (map[i / n][i % n] == 'S') cnt++;
+    for (uint32_t i = 0; i < E->S; ++i) E->start[i] = map[i / n][i % n] == 'S' ? 1.0 / (double)cnt : 0.0;
+    E->n_start = E->S;
+    for (uint32_t row = 0; row < n; ++row)
+        for (uint32_t col = 0; col < n; ++col) {
+            uint32_t s = row * n + col;
+            for (uint32_t a = 0; a < 4; ++a) {
+                for (int i = 0; i < 3; ++i) set_outcome(E, s, a, i, 0.0, 0, 0.0, 0);
+                char letter = map[row][col];
+                if (letter == 'G' || letter == 'H') {
+                    set_outcome(E, s, a, 0, 1.0, s, 0.0, 1);
+                } else {
+                    /* slippery: [(a-1)%4, a, (a+1)%4] with usize wrap (release): a=0 -> 3 */
+                    uint32_t bs[3] = {(a + 3) % 4, a, (a + 1) % 4};
+                    int nb = slippery ? 3 : 1;
+                    for (int i = 0; i < nb; ++i) {
+                        uint32_t b = slippery ? bs[i] : a;
+                        uint32_t nr, nc;
+                        inc(n, n, row, col, b, &nr, &nc);           /* update_probability_matrix :30-44 */
+                        char nl = map[nr][nc];
+                        int t = nl == 'G' || nl == 'H';
+                        double r = nl == 'G' ? 1.0 : 0.0;
+                        set_outcome(E, s, a, i, slippery ? 1.0 / 3.0 : 1.0, nr * n + nc, r, t);
+                    }
+                }
+            }
+        }
+    E->trunc_reward = 0.0; /* frozen_lake.rs:119-122 */
+}
+
+/* CliffWalkingEnv::new: src/env/cliff_walking.rs:22-58 */
+static void build_cliff_walking(envdef *E) {
+    E->S = 48; E->A = 4;
+    for (uint32_t row = 0; row < 4; ++row)
+        for (uint32_t col = 0; col < 12; ++col)
+            for (uint32_t a = 0; a < 4; ++a) {
+                uint32_t nr, nc;
+                inc(4, 12, row, col, a, &nr, &nc);
+                uint32_t ns = nr * 12 + nc;
+                int win = ns == 47, lose = ns >= 37 && ns <= 46;
+                for (int i = 0; i < 3; ++i) set_outcome(E, row * 12 + col, a, i, 0.0, 0, 0.0, 0);
+                set_outcome(E, row * 12 + col, a, 0, 1.0, ns, lose ? -100.0 : -1.0, lose || win);
+            }
+    for (uint32_t i = 0; i < 48; ++i) E->start[i] = i == 36 ? 1.0 : 0.0;
+    E->n_start = 48;
+    E->trunc_reward = -100.0; /* cliff_walking.rs:81-84 */
+}
+
+/* TaxiEnv::new: src/env/taxi.rs:57-131 */
+static void build_taxi(envdef *E) {
+    E->S = 500; E->A = 6;
+    double sum = 0.0;
+    for (uint32_t i = 0; i < 500; ++i) E->start[i] = 0.0;
+    for (uint32_t row = 0; row < 5; ++row)
+        for (uint32_t col = 0; col < 5; ++col)
+            for (uint32_t pass = 0; pass < 5; ++pass)
+                for (uint32_t dest = 0; dest < 4; ++dest) {
+                    uint32_t state = ((row * 5 + col) * 5 + pass) * 4 + dest;   /* encode :33-42 */
+                    if (pass < 4 && pass != dest) { E->start[state] += 1.0; sum += 1.0; }
+                    for (uint32_t action = 0; action < 6; ++action) {
+                        uint32_t nrow = row, ncol = col, npass = pass;
+                        double reward = -1.0;
+                        int term = 0;
+                        if (action == 0) nrow = row + 1 < 4 ? row + 1 : 4;
+                        else if (action == 1) nrow = row != 0 ? row - 1 : 0;
+                        if (action == 2 && TAXI_MAP[1 + row][2 * col + 2] == ':') {
+                            ncol = col + 1 < 4 ? col + 1 : 4;
+                        } else if (action == 3 && TAXI_MAP[1 + row][2 * col] == ':') {
+                            ncol = col != 0 ? col - 1 : 0;
+                        } else if (action == 4) {
+                            if (pass < 4 && row == TAXI_LOCS[pass][0] && col == TAXI_LOCS[pass][1]) npass = 4;
+                            else reward = -10.0;
+                        } else if (action == 5) {
+                            if (row == TAXI_LOCS[dest][0] && col == TAXI_LOCS[dest][1] && pass == 4) {
+                                npass = dest; term = 1; reward = 20.0;
+                            } else reward = -10.0;
+                        }
+                        uint32_t ns = ((nrow * 5 + ncol) * 5 + npass) * 4 + dest;
+                        for (int i = 0; i < 3; ++i) set_outcome(E, state, action, i, 0.0, 0, 0.0, 0);
+                        set_outcome(E, state, action, 0, 1.0, ns, reward, term);
+                    }
+                }
+    for (uint32_t i = 0; i < 500; ++i) E->start[i] /= sum;    /* :117-119 */
+    E->n_start = 500;
+    E->trunc_reward = 0.0; /* taxi.rs:146-149 */
+}
+
+static int build_env(envdef *E, const rlo_config *c) {
+    memset(E, 0, sizeof(*E));
+    E->kind = c->env;
+    E->max_steps = c->max_steps;
+    switch (c->env) {
+    case RLO_ENV_FROZEN_LAKE: build_frozen_lake(E, c->map8x8, c->slippery); return 0;
+    case RLO_ENV_CLIFF_WALKING: build_cliff_walking(E); return 0;
+    case RLO_ENV_TAXI: build_taxi(E); return 0;
+    case RLO_ENV_BLACKJACK: E->S = 32 * 32 * 2; E->A = 2; return 0;
+    }
+    return -1;
+}
+
+int rlo_env_dims(const rlo_config *c, uint32_t *S, uint32_t *A) {
+    static envdef E;
+    if (build_env(&E, c)) return -1;
+    *S = E.S; *A = E.A;
+    return 0;
+}
+int rlo_env_table(const rlo_config *c, double *prob, uint32_t *next, double *reward, uint8_t *term) {
+    static envdef E;
+    if (build_env(&E, c) || c->env == RLO_ENV_BLACKJACK) return -1;
+    size_t n = (size_t)E.S * E.A * 3;
+    memcpy(prob, E.prob, n * sizeof(double));
+    memcpy(next, E.next, n * sizeof(uint32_t));
+    memcpy(reward, E.rew, n * sizeof(double));
+    memcpy(term, E.term, n);
+    return 0;
+}
+int rlo_env_start(const rlo_config *c, double *start) {
+    static envdef E;
+    if (build_env(&E, c) || c->env == RLO_ENV_BLACKJACK) return -1;
+    memcpy(start, E.start, E.S * sizeof(double));
+    return 0;
+}
+
+/* blackjack helpers: src/env/blackjack.rs:47-83 */
+static inline uint32_t bj_score(uint32_t sum, uint32_t ace) { return (ace && sum + 10 <= 21) ? sum + 10 : sum; }
+static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 32 + d) * 2 + (ace ? 1 : 0); }
+static void bj_initialize_hands(envstate *st, rlo_rng *r) {       /* :47-56 */
+    uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
+    st->p_sum = p0 + p1; st->d_sum = d0 + d1; st->d0 = d0;
+    st->p_ace = p0 == 1 || p1 == 1;
+    st->d_ace = d0 == 1 || d1 == 1;
+}
+
+/* Env::reset: frozen_lake.rs:106-113, cliff_walking.rs:70-75, taxi.rs:135-142, blackjack.rs:105-116 */
+static uint32_t env_reset(const envdef *E, envstate *st, rlo_rng *r) {
+    if (E->kind == RLO_ENV_BLACKJACK) {
+        bj_initialize_hands(st, r);
+        st->ready = 1;
+        return bj_index(bj_score(st->p_sum, st->p_ace), st->d0, st->p_ace);
+    }
+    if (E->kind == RLO_ENV_CLIFF_WALKING) {
+        st->pos = 36;
+    } else {
+        double u = uniform01(r);
+        st->pos = categorical_sample(E->start, E->n_start, u);
+    }
+    st->ready = 1;
+    st->curr_step = 0;
+    return st->pos;
+}
+
+/* Env::step: frozen_lake.rs:115-134, cliff_walking.rs:77-91, taxi.rs:144-159,
+ * blackjack.rs:118-163.  Returns -1 (EnvNotReady) if not ready. */
+static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint32_t *s2, double *rew,
+                    int *term) {
+    if (!st->ready) return -1;
+    if (E->kind == RLO_ENV_BLACKJACK) {
+        if (a == 0) {                                   /* hit :121-138 */
+            st->p_sum += draw_card(r);
+            uint32_t p = bj_score(st->p_sum, st->p_ace);
+            if (p > 21) {
+                st->ready = 0;
+                *s2 = bj_index(p, bj_score(st->d_sum, st->d_ace), st->p_ace);
+                *rew = -1.0; *term = 1;
+                return 0;
+            }
+            *s2 = bj_index(p, st->d0, st->p_ace);
+            *rew = 0.0; *term = 0;
+            return 0;
+        }
+        st->ready = 0;                                  /* stick :139-162 */
+        uint32_t d = bj_score(st->d_sum, st->d_ace);
+        while (d < 17) {
+            st->d_sum += draw_card(r);
+            d = bj_score(st->d_sum, st->d_ace);
+        }
+        uint32_t p = bj_score(st->p_sum, st->p_ace);
+        *s2 = bj_index(p, d, st->p_ace);
+        *term = 1;
+        if (d > 21) *rew = 1.0;
+        else *rew = p > d ? 1.0 : (p < d ? -1.0 : 0.0);
+        return 0;
+    }
+    if (st->curr_step >= E->max_steps) {            /* truncation: (0, r_trunc, true) */
+        st->ready = 0;
+        *s2 = 0; *rew = E->trunc_reward; *term = 1;
+        return 0;
+    }
+    st->curr_step += 1;
+    size_t k = ((size_t)st->pos * E->A + a) * 3;
+    uint32_t i = 0;
+    if (E->kind == RLO_ENV_FROZEN_LAKE) {
+        double u = uniform01(r);                       /* one draw even when not slippery */
+        i = categorical_sample(&E->prob[k], 3, u);
+    }
+    st->pos = E->next[k + i];
+    *s2 = st->pos; *rew = E->rew[k + i]; *term = E->term[k + i];
+    if (*term) st->ready = 0;
+    return 0;
+}
+
+/* ======================================================================== */
+/* action selection & TD targets (shared by both restatements)              */
+/* ======================================================================== */
+/* UpperConfidenceBound ucbs: upper_confidence_bound.rs:29-37,53-57 */
+static inline double ucb_value(double q, double c, double lnt, double n) {
+    return q + c * sqrt(lnt / (n + MIN_POSITIVE));
+}
+/* UniformEpsilonGreed::get_exploration_probs: uniform_epsilon_greed.rs:72-76 */
+static void eps_probs(double eps, const double *q, uint32_t A, double *p) {
+    for (uint32_t i = 0; i < A; ++i) p[i] = eps / (double)A;
+    p[argmax_d(q, A)] = 1.0 - eps;
+}
+/* UCB get_exploration_probs: upper_confidence_bound.rs:48-63 */
+static void ucb_probs(const double *q, const uint64_t *n, uint64_t t, double c, uint32_t A, double *p) {
+    double lnt = rlo_log((double)t);
+    double sum = 0.0;
+    for (uint32_t i = 0; i < A; ++i) {
+        p[i] = ucb_value(q[i], c, lnt, (double)n[i]);
+        sum += p[i];
+    }
+    for (uint32_t i = 0; i < A; ++i) p[i] /= sum;
+}
+/* sarsa / qlearning / expected_sarsa: src/agent.rs:19-45 */
+static double future_q(int algo, const double *q2, uint32_t a2, const double *p, uint32_t A) {
+    if (algo == RLO_ALGO_SARSA) return q2[a2];
+    if (algo == RLO_ALGO_QLEARNING) return max_d(q2, A);
+    double f = 0.0;
+    for (uint32_t i = 0; i < A; ++i) f += p[i] * q2[i];
+    return f;
+}
+/* decay_epsilon: uniform_epsilon_greed.rs:42-49 with the bins' closure
+ * `a - epsilon_decay` (src/bin/frozen_lake.rs:84,146) or `a * d` (frozen_lake_neural.rs:181) */
+static double decay_eps(const rlo_config *c, double eps) {
+    double nw = c->decay_kind == RLO_DECAY_MUL ? eps * c->eps_decay : eps - c->eps_decay;
+    return c->eps_final > nw ? eps : nw;
+}
+
+/* ======================================================================== */
+/* 1. faithful single-env restatement                                        */
+/* ======================================================================== */
+typedef struct { void *p; size_t n, cap, esz; } vec;
+static void vpush(vec *v, const void *x) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 1024;
+        v->p = realloc(v->p, v->cap * v->esz);
+    }
+    memcpy((char *)v->p + v->n * v->esz, x, v->esz);
+    v->n++;
+}
+
+struct rlo_faithful {
+    rlo_config c;
+    envdef E;
+    envstate st;
+    rlo_rng rng;
+    uint32_t S, A, P;
+    double *q;           /* [P][S][A] f64 */
+    int dflag;           /* DoubleTabularPolicy::policy_flag (starts true) */
+    double eps;
+    uint64_t *ucb_n;     /* [S][A] (u128 in the reference) */
+    uint64_t ucb_t;
+    double *trace;       /* [S][A] */
+    uint8_t *visited;    /* [S] — membership of the trace FxHashMap */
+    vec reward_history, episode_length, training_error, records;
+    int record;
+};
+
+static void f_clear_policy(rlo_faithful *f) {
+    for (size_t i = 0; i < (size_t)f->P * f->S * f->A; ++i) f->q[i] = f->c.q_default;
+}
+static void f_reset_selector(rlo_faithful *f) {
+    f->eps = f->c.eps0;
+    memset(f->ucb_n, 0, sizeof(uint64_t) * f->S * f->A);
+    f->ucb_t = 1;
+}
+
+rlo_faithful *rlo_faithful_create(const rlo_config *c) {
+    rlo_faithful *f = (rlo_faithful *)calloc(1, sizeof(rlo_faithful));
+    f->c = *c;
+    if (build_env(&f->E, c)) { free(f); return NULL; }
+    f->S = f->E.S; f->A = f->E.A; f->P = c->policy == RLO_POLICY_DOUBLE ? 2 : 1;
+    f->q = (double *)malloc(sizeof(double) * f->P * f->S * f->A);
+    f->ucb_n = (uint64_t *)calloc((size_t)f->S * f->A, sizeof(uint64_t));
+    f->trace = (double *)calloc((size_t)f->S * f->A, sizeof(double));
+    f->visited = (uint8_t *)calloc(f->S, 1);
+    f->reward_history.esz = sizeof(double);
+    f->episode_length.esz = sizeof(uint64_t);
+    f->training_error.esz = sizeof(double);
+    f->records.esz = sizeof(rlo_record);
+    f->dflag = 1;
+    f_clear_policy(f);
+    f_reset_selector(f);
+    rng_seed(&f->rng, c->seed, c->lane_offset);
+    if (c->env == RLO_ENV_BLACKJACK) bj_initialize_hands(&f->st, &f->rng); /* BlackJackEnv::new deals */
+    return f;
+}
+void rlo_faithful_destroy(rlo_faithful *f) {
+    if (!f) return;
+    free(f->q); free(f->ucb_n); free(f->trace); free(f->visited);
+    free(f->reward_history.p); free(f->episode_length.p); free(f->training_error.p); free(f->records.p);
+    free(f);
+}
+void rlo_faithful_set_record(rlo_faithful *f, int e) { f->record = e; }
+double rlo_faithful_epsilon(const rlo_faithful *f) { return f->eps; }
+
+/* Policy::predict: tabular_policy.rs:27-29, double_tabular_policy.rs:31-40 */
+static void f_predict(const rlo_faithful *f, uint32_t s, double *out) {
+    const double *a = &f->q[(size_t)s * f->A];
+    if (f->P == 1) { for (uint32_t i = 0; i < f->A; ++i) out[i] = a[i]; return; }
+    const double *b = &f->q[((size_t)f->S + s) * f->A];
+    for (uint32_t i = 0; i < f->A; ++i) out[i] = (a[i] + b[i]) / 2.0;
+}
+/* Policy::get_values: tabular_policy.rs:31-33, double_tabular_policy.rs:42-50 (flag ? alpha : beta) */
+static const double *f_values(const rlo_faithful *f, uint32_t s) {
+    uint32_t tbl = (f->P == 2 && !f->dflag) ? 1 : 0;
+    return &f->q[((size_t)tbl * f->S + s) * f->A];
+}
+/* Policy::update: tabular_policy.rs:35-38, double_tabular_policy.rs:52-60 (flag ? beta : alpha) */
+static void f_policy_update(rlo_faithful *f, uint32_t s, uint32_t a, double td) {
+    uint32_t tbl = (f->P == 2 && f->dflag) ? 1 : 0;
+    f->q[((size_t)tbl * f->S + s) * f->A + a] += f->c.lr * td;
+}
+/* Agent::get_action: one_step_agent.rs:48-51 / elegibility_traces_agent.rs:56-59 */
+static uint32_t f_get_action(rlo_faithful *f, uint32_t s) {
+    double v[MAXA];
+    f_predict(f, s, v);
+    if (f->c.selector == RLO_SEL_EPS_GREEDY) {             /* uniform_epsilon_greed.rs:60-66 */
+        if (f->eps != 0.0 && uniform01(&f->rng) < f->eps) return uniform_action(&f->rng, f->A);
+        return argmax_d(v, f->A);
+    }
+    uint64_t *n = &f->ucb_n[(size_t)s * f->A];             /* upper_confidence_bound.rs:29-42 */
+    double lnt = rlo_log((double)f->ucb_t);
+    double u[MAXA];
+    for (uint32_t i = 0; i < f->A; ++i) u[i] = ucb_value(v[i], f->c.ucb_c, lnt, (double)n[i]);
+    uint32_t a = argmax_d(u, f->A);
+    n[a] += 1;
+    f->ucb_t += 1;
+    return a;
+}
+/* Agent::update: one_step_agent.rs:53-86 and elegibility_traces_agent.rs:61-104 */
+static double f_update(rlo_faithful *f, uint32_t s, uint32_t a, double r, int term, uint32_t s2,
+                       uint32_t a2) {
+    const uint32_t A = f->A;
+    double q2[MAXA], p[MAXA], q[MAXA];
+    memcpy(q2, f_values(f, s2), A * sizeof(double));
+    if (f->c.selector == RLO_SEL_EPS_GREEDY) eps_probs(f->eps, q2, A, p);
+    else ucb_probs(q2, &f->ucb_n[(size_t)s2 * A], f->ucb_t, f->c.ucb_c, A, p);
+    double fq = future_q(f->c.algo, q2, a2, p, A);
+    memcpy(q, f_values(f, s), A * sizeof(double));
+    double td = r + f->c.gamma * fq - q[a];
+    if (f->c.agent == RLO_AGENT_ONE_STEP) {
+        f_policy_update(f, s, a, td);
+    } else {
+        f->trace[(size_t)s * A + a] += 1.0;
+        f->visited[s] = 1;
+        for (uint32_t o = 0; o < f->S; ++o) {
+            if (!f->visited[o]) continue;
+            for (uint32_t b = 0; b < A; ++b) {
+                double *e = &f->trace[(size_t)o * A + b];
+                f_policy_update(f, o, b, td * *e);
+                *e *= f->c.gamma * f->c.lambda_;
+            }
+        }
+    }
+    if (f->P == 2) f->dflag = !f->dflag;                   /* after_update */
+    if (term) {
+        if (f->c.agent == RLO_AGENT_TRACES) {
+            memset(f->trace, 0, sizeof(double) * f->S * A);
+            memset(f->visited, 0, f->S);
+        }
+        if (f->c.selector == RLO_SEL_EPS_GREEDY) f->eps = decay_eps(&f->c, f->eps);
+    }
+    return td;
+}
+
+/* Agent::evaluate: src/agent.rs:120-141 */
+uint64_t rlo_faithful_evaluate(rlo_faithful *f, uint64_t n_episodes) {
+    uint64_t steps = 0;
+    for (uint64_t ep = 0; ep < n_episodes; ++ep) {
+        uint32_t a = f_get_action(f, env_reset(&f->E, &f->st, &f->rng));
+        for (;;) {
+            uint32_t s2; double r; int term;
+            if (env_step(&f->E, &f->st, a, &f->rng, &s2, &r, &term)) abort(); /* unwrap */
+            steps++;
+            a = f_get_action(f, s2);
+            if (term) break;
+        }
+    }
+    return steps;
+}
+
+/* Agent::train: src/agent.rs:66-118 */
+uint64_t rlo_faithful_train(rlo_faithful *f, uint64_t n_episodes, uint64_t eval_at) {
+    f->reward_history.n = f->episode_length.n = f->training_error.n = f->records.n = 0;
+    uint64_t steps = 0;
+    for (uint64_t episode = 0; episode < n_episodes; ++episode) {
+        uint64_t action_counter = 0;
+        double epi_reward = 0.0;
+        uint32_t s = env_reset(&f->E, &f->st, &f->rng);
+        uint32_t a = f_get_action(f, s);
+        for (;;) {
+            action_counter++;
+            uint32_t s2; double r; int term;
+            if (env_step(&f->E, &f->st, a, &f->rng, &s2, &r, &term)) abort();
+            uint32_t a2 = f_get_action(f, s2);
+            double td = f_update(f, s, a, r, term, s2, a2);
+            vpush(&f->training_error, &td);
+            if (f->record) {
+                rlo_record rec;
+                memset(&rec, 0, sizeof rec);
+                rec.s = s; rec.a = (uint8_t)a; rec.s2 = s2; rec.a2 = (uint8_t)a2;
+                rec.r = r; rec.term = (uint8_t)term; rec.td = td; rec.mode = RLO_MODE_TRAIN;
+                vpush(&f->records, &rec);
+            }
+            steps++;
+            s = s2; a = a2;
+            epi_reward += r;
+            if (term) { vpush(&f->reward_history, &epi_reward); break; }
+        }
+        if (eval_at && episode % eval_at == 0) rlo_faithful_evaluate(f, f->c.eval_episodes);
+        vpush(&f->episode_length, &action_counter);
+    }
+    return steps;
+}
+/* Agent::reset (one_step_agent.rs:43-46): selector.reset + policy.reset (flag kept) */
+void rlo_faithful_reset(rlo_faithful *f) { f_reset_selector(f); f_clear_policy(f); }
+void rlo_faithful_get_q(const rlo_faithful *f, double *out) {
+    memcpy(out, f->q, sizeof(double) * f->P * f->S * f->A);
+}
+uint64_t rlo_faithful_n_episodes(const rlo_faithful *f) { return f->reward_history.n; }
+uint64_t rlo_faithful_n_steps(const rlo_faithful *f) { return f->training_error.n; }
+void rlo_faithful_histories(const rlo_faithful *f, double *rh, uint64_t *el, double *te) {
+    if (rh) memcpy(rh, f->reward_history.p, f->reward_history.n * sizeof(double));
+    if (el) memcpy(el, f->episode_length.p, f->episode_length.n * sizeof(uint64_t));
+    if (te) memcpy(te, f->training_error.p, f->training_error.n * sizeof(double));
+}
+uint64_t rlo_faithful_get_records(const rlo_faithful *f, rlo_record *out, uint64_t cap) {
+    uint64_t n = f->records.n < cap ? f->records.n : cap;
+    memcpy(out, f->records.p, n * sizeof(rlo_record));
+    return f->records.n;
+}
+uint64_t rlo_faithful_bench(const rlo_config *c, uint64_t n_episodes, uint64_t eval_at, double *sec) {
+    rlo_faithful *f = rlo_faithful_create(c);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    uint64_t steps = rlo_faithful_train(f, n_episodes, eval_at);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    *sec = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    rlo_faithful_destroy(f);
+    return steps;
+}
+
+/* ======================================================================== */
+/* 2. batched schedule (the GPU semantics) — fixed-point Q                   */
+/*                                                                           */
+/* Per learner group g (lanes [g*G, (g+1)*G)) and synchronous step:          */
+/*   R-phase: lanes needing a reset: s=reset(), a=get_action(s)              */
+/*            (UCB: all read N,t; then N[s][a]+=1 per lane, t+=#calls)       */
+/*   S-phase: (s2,r,term)=step(a); a2=get_action(s2) (same UCB snapshot rule) */
+/*            train lanes: td from the Q snapshot, deltas summed, applied at  */
+/*            the end of the step (integer sums: order-free).                */
+/* Every K=sync_every steps: Q_base += sum_g (Q_g - Q_base), same for N, t.  */
+/* ======================================================================== */
+typedef struct {
+    rlo_rng rng;
+    envstate st;
+    uint32_t s, a;
+    int need_reset, dflag, mode;
+    double eps, epi_reward;
+    uint64_t train_ep, eval_left, epi_len;
+    double *trace;       /* [S][A] (traces agent) */
+    uint8_t *visited;
+    /* private mode (G == 1): the lane is a whole reference agent */
+    double *qd;          /* [P][S][A] f64 */
+    uint32_t *n;         /* [S][A] */
+    uint64_t t;
+} lane_t;
+
+struct rlo_batch {
+    rlo_config c;
+    envdef E;
+    uint32_t S, A, P, G, n_groups, K;
+    int specials;        /* UCB + expected SARSA can produce inf/NaN */
+    int priv;            /* G == 1: private f64 Q per lane, no merging */
+    double *qd_g;        /* private mode: current lane's Q */
+    int64_t *q_base;     /* [P][S][A] */
+    uint8_t *f_base;
+    uint32_t *n_base;    /* [S][A] */
+    uint64_t t_base;
+    /* current group scratch */
+    int64_t *q_g, *dq;
+    uint8_t *f_g, *df;
+    uint32_t *n_g, *n_g_own;
+    uint64_t t_g;
+    /* merge accumulators */
+    int64_t *acc_q; uint8_t *acc_f; int64_t *acc_n; int64_t acc_t;
+    lane_t *lanes;
+    uint64_t target_episodes, eval_at;
+    int eval_only;
+    int record;
+    vec records;
+    uint64_t stats[8];
+};
+
+static int64_t q_fix(double d, uint8_t *flag) {
+    if (d != d) { *flag |= QF_NAN; return 0; }
+    if (d == INFINITY) { *flag |= QF_PINF; return 0; }
+    if (d == -INFINITY) { *flag |= QF_NINF; return 0; }
+    double x = d * 0x1p40;
+    if (x >= 0x1p62) return (int64_t)1 << 62;
+    if (x <= -0x1p62) return -((int64_t)1 << 62);
+    return (int64_t)rint(x);
+}
+static inline double q_val(int64_t raw, uint8_t fl) {
+    if (fl) {
+        if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return NAN;
+        return (fl & QF_PINF) ? INFINITY : -INFINITY;
+    }
+    return (double)raw * 0x1p-40;
+}
+static inline int64_t wrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+
+static void b_row(const rlo_batch *b, uint32_t tbl, uint32_t s, double *out) {
+    size_t base = ((size_t)tbl * b->S + s) * b->A;
+    if (b->priv) {
+        for (uint32_t i = 0; i < b->A; ++i) out[i] = b->qd_g[base + i];
+        return;
+    }
+    for (uint32_t i = 0; i < b->A; ++i) out[i] = q_val(b->q_g[base + i], b->f_g[base + i]);
+}
+static void b_predict(const rlo_batch *b, uint32_t s, double *out) {
+    b_row(b, 0, s, out);
+    if (b->P == 2) {
+        double o2[MAXA];
+        b_row(b, 1, s, o2);
+        for (uint32_t i = 0; i < b->A; ++i) out[i] = (out[i] + o2[i]) / 2.0;
+    }
+}
+/* get_action against the group snapshot; UCB increments are returned, not applied */
+static uint32_t b_select(rlo_batch *b, lane_t *L, uint32_t s) {
+    double v[MAXA];
+    b_predict(b, s, v);
+    if (b->c.selector == RLO_SEL_EPS_GREEDY) {
+        if (L->eps != 0.0 && uniform01(&L->rng) < L->eps) return uniform_action(&L->rng, b->A);
+        return argmax_d(v, b->A);
+    }
+    const uint32_t *n = &b->n_g[(size_t)s * b->A];
+    double lnt = rlo_log((double)b->t_g);
+    double u[MAXA];
+    for (uint32_t i = 0; i < b->A; ++i) u[i] = ucb_value(v[i], b->c.ucb_c, lnt, (double)n[i]);
+    return argmax_d(u, b->A);
+}
+
+static void lane_init(rlo_batch *b, lane_t *L, uint64_t gid) {
+    memset(&L->st, 0, sizeof L->st);
+    rng_seed(&L->rng, b->c.seed, gid);
+    if (b->c.env == RLO_ENV_BLACKJACK) bj_initialize_hands(&L->st, &L->rng);
+    L->need_reset = 1; L->dflag = 1; L->mode = RLO_MODE_TRAIN;
+    L->eps = b->c.eps0;
+    L->train_ep = L->eval_left = L->epi_len = 0;
+    L->epi_reward = 0.0;
+    L->s = L->a = 0;
+}
+
+rlo_batch *rlo_batch_create(const rlo_config *c) {
+    rlo_batch *b = (rlo_batch *)calloc(1, sizeof(rlo_batch));
+    b->c = *c;
+    if (build_env(&b->E, c) || c->n_lanes == 0 || c->group_size == 0 || c->sync_every == 0) {
+        free(b);
+        return NULL;
+    }
+    b->S = b->E.S; b->A = b->E.A; b->P = c->policy == RLO_POLICY_DOUBLE ? 2 : 1;
+    b->G = c->group_size; b->K = c->sync_every;
+    b->n_groups = (c->n_lanes + b->G - 1) / b->G;
+    b->specials = c->selector == RLO_SEL_UCB && c->algo == RLO_ALGO_EXPECTED_SARSA;
+    b->priv = b->G == 1;
+    if (b->G > 1024) { free(b); return NULL; }
+    size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
+    b->q_base = (int64_t *)malloc(nq * 8); b->f_base = (uint8_t *)calloc(nq, 1);
+    b->q_g = (int64_t *)malloc(nq * 8); b->f_g = (uint8_t *)calloc(nq, 1);
+    b->dq = (int64_t *)calloc(nq, 8); b->df = (uint8_t *)calloc(nq, 1);
+    b->acc_q = (int64_t *)calloc(nq, 8); b->acc_f = (uint8_t *)calloc(nq, 1);
+    b->n_base = (uint32_t *)calloc(nsa, 4); b->n_g = b->n_g_own = (uint32_t *)calloc(nsa, 4);
+    b->acc_n = (int64_t *)calloc(nsa, 8);
+    b->records.esz = sizeof(rlo_record);
+    b->lanes = (lane_t *)calloc(c->n_lanes, sizeof(lane_t));
+    for (uint32_t i = 0; i < c->n_lanes; ++i) {
+        if (c->agent == RLO_AGENT_TRACES) {
+            b->lanes[i].trace = (double *)calloc(nsa, sizeof(double));
+            b->lanes[i].visited = (uint8_t *)calloc(b->S, 1);
+        }
+        if (b->priv) {
+            b->lanes[i].qd = (double *)malloc(nq * sizeof(double));
+            b->lanes[i].n = (uint32_t *)calloc(nsa, sizeof(uint32_t));
+        }
+        lane_init(b, &b->lanes[i], c->lane_offset + i);
+    }
+    rlo_batch_reset(b);
+    return b;
+}
+void rlo_batch_destroy(rlo_batch *b) {
+    if (!b) return;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        free(b->lanes[i].trace); free(b->lanes[i].visited); free(b->lanes[i].qd); free(b->lanes[i].n);
+    }
+    free(b->lanes); free(b->q_base); free(b->f_base); free(b->q_g); free(b->f_g); free(b->dq);
+    free(b->df); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
+    free(b->records.p);
+    free(b);
+}
+/* Agent::reset: policy cleared to the default row, selector state fresh, lane
+ * ε restored; env/RNG/double-flag untouched (one_step_agent.rs:43-46,
+ * double_tabular_policy.rs:62-65 keeps policy_flag). */
+void rlo_batch_reset(rlo_batch *b) {
+    size_t nq = (size_t)b->P * b->S * b->A;
+    uint8_t fl = 0;
+    int64_t d = q_fix(b->c.q_default, &fl);
+    for (size_t i = 0; i < nq; ++i) { b->q_base[i] = d; b->f_base[i] = fl; }
+    memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
+    b->t_base = 1;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        lane_t *L = &b->lanes[i];
+        L->eps = b->c.eps0;
+        if (b->priv) {
+            for (size_t k = 0; k < nq; ++k) L->qd[k] = b->c.q_default;
+            memset(L->n, 0, sizeof(uint32_t) * b->S * b->A);
+            L->t = 1;
+        }
+    }
+}
+void rlo_batch_set_selector(rlo_batch *b, int32_t sel) {
+    b->c.selector = sel;
+    b->specials = b->c.selector == RLO_SEL_UCB && b->c.algo == RLO_ALGO_EXPECTED_SARSA;
+    memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
+    b->t_base = 1;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        b->lanes[i].eps = b->c.eps0;
+        if (b->priv) { memset(b->lanes[i].n, 0, sizeof(uint32_t) * b->S * b->A); b->lanes[i].t = 1; }
+    }
+}
+void rlo_batch_set_algo(rlo_batch *b, int32_t algo) {
+    b->c.algo = algo;
+    b->specials = b->c.selector == RLO_SEL_UCB && b->c.algo == RLO_ALGO_EXPECTED_SARSA;
+}
+void rlo_batch_set_record(rlo_batch *b, int e) { b->record = e; }
+
+static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double delta) {
+    size_t k = ((size_t)tbl * b->S + s) * b->A + a;
+    if (b->priv) {                   /* Q[s][a] += lr*td exactly as tabular_policy.rs:36 */
+        b->qd_g[k] += delta;
+        return;
+    }
+    uint8_t fl = 0;
+    int64_t d = q_fix(delta, &fl);
+    b->dq[k] = wrap_add(b->dq[k], d);
+    b->df[k] |= fl;
+}
+
+static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *rec) {
+    const uint32_t A = b->A;
+    const int ucb = b->c.selector == RLO_SEL_UCB;
+    uint32_t sel_s[1024], sel_a[1024];
+    uint32_t nsel = 0;
+    /* ---- R-phase ---- */
+    for (uint32_t j = 0; j < nl; ++j) {
+        lane_t *L = &b->lanes[lane0 + j];
+        if (L->mode == RLO_MODE_DONE || !L->need_reset) continue;
+        L->s = env_reset(&b->E, &L->st, &L->rng);
+        L->a = b_select(b, L, L->s);
+        L->need_reset = 0; L->epi_reward = 0.0; L->epi_len = 0;
+        if (ucb) { sel_s[nsel] = L->s; sel_a[nsel] = L->a; nsel++; }
+    }
+    for (uint32_t i = 0; i < nsel; ++i) b->n_g[(size_t)sel_s[i] * A + sel_a[i]] += 1;
+    b->t_g += nsel;
+    nsel = 0;
+    /* ---- S-phase: env step + next action ---- */
+    uint32_t s2v[1024], a2v[1024];
+    double rv[1024];
+    int tv[1024];
+    for (uint32_t j = 0; j < nl; ++j) {
+        lane_t *L = &b->lanes[lane0 + j];
+        if (L->mode == RLO_MODE_DONE) continue;
+        if (env_step(&b->E, &L->st, L->a, &L->rng, &s2v[j], &rv[j], &tv[j])) abort();
+        a2v[j] = b_select(b, L, s2v[j]);
+        if (ucb) { sel_s[nsel] = s2v[j]; sel_a[nsel] = a2v[j]; nsel++; }
+    }
+    for (uint32_t i = 0; i < nsel; ++i) b->n_g[(size_t)sel_s[i] * A + sel_a[i]] += 1;
+    b->t_g += nsel;
+    /* ---- S-phase: TD update against the Q snapshot ---- */
+    size_t nq = (size_t)b->P * b->S * A;
+    memset(b->dq, 0, nq * 8);
+    memset(b->df, 0, nq);
+    for (uint32_t j = 0; j < nl; ++j) {
+        lane_t *L = &b->lanes[lane0 + j];
+        rlo_record *R = rec ? &rec[j] : NULL;
+        if (R) { memset(R, 0, sizeof *R); R->mode = (uint8_t)L->mode; }
+        if (L->mode == RLO_MODE_DONE) continue;
+        uint32_t s = L->s, a = L->a, s2 = s2v[j], a2 = a2v[j];
+        double r = rv[j];
+        int term = tv[j];
+        double td = 0.0;
+        if (L->mode == RLO_MODE_TRAIN) {
+            uint32_t vt = (b->P == 2 && !L->dflag) ? 1 : 0;   /* get_values table */
+            uint32_t ut = (b->P == 2 && L->dflag) ? 1 : 0;    /* update table */
+            double q2[MAXA], p[MAXA], q[MAXA];
+            b_row(b, vt, s2, q2);
+            if (!ucb) eps_probs(L->eps, q2, A, p);
+            else if (b->c.algo == RLO_ALGO_EXPECTED_SARSA) {
+                uint64_t n64[MAXA];
+                for (uint32_t i = 0; i < A; ++i) n64[i] = b->n_g[(size_t)s2 * A + i];
+                ucb_probs(q2, n64, b->t_g, b->c.ucb_c, A, p);
+            }
+            double fq = future_q(b->c.algo, q2, a2, p, A);
+            b_row(b, vt, s, q);
+            td = r + b->c.gamma * fq - q[a];
+            if (b->c.agent == RLO_AGENT_ONE_STEP) {
+                add_delta(b, ut, s, a, b->c.lr * td);
+            } else {
+                L->trace[(size_t)s * A + a] += 1.0;
+                L->visited[s] = 1;
+                for (uint32_t o = 0; o < b->S; ++o) {
+                    if (!L->visited[o]) continue;
+                    for (uint32_t bb = 0; bb < A; ++bb) {
+                        double *e = &L->trace[(size_t)o * A + bb];
+                        add_delta(b, ut, o, bb, b->c.lr * (td * *e));
+                        *e *= b->c.gamma * b->c.lambda_;
+                    }
+                }
+            }
+            if (b->P == 2) L->dflag = !L->dflag;
+            if (term) {
+                if (b->c.agent == RLO_AGENT_TRACES) {
+                    memset(L->trace, 0, sizeof(double) * b->S * A);
+                    memset(L->visited, 0, b->S);
+                }
+                if (!ucb) L->eps = decay_eps(&b->c, L->eps);
+            }
+            b->stats[0]++;
+        } else {
+            b->stats[1]++;
+        }
+        if (R) {
+            R->s = s; R->a = (uint8_t)a; R->s2 = s2; R->a2 = (uint8_t)a2;
+            R->r = r; R->term = (uint8_t)term; R->td = td;
+        }
+        /* bookkeeping: src/agent.rs:98-116 */
+        L->epi_reward += r;
+        L->epi_len++;
+        L->s = s2; L->a = a2;
+        if (term) {
+            L->need_reset = 1;
+            if (L->mode == RLO_MODE_TRAIN) {
+                uint64_t ep = L->train_ep++;
+                b->stats[2]++;
+                b->stats[4] += (uint64_t)(int64_t)rint(L->epi_reward * 65536.0);
+                if (b->eval_at && ep % b->eval_at == 0) {
+                    L->mode = RLO_MODE_EVAL;
+                    L->eval_left = b->c.eval_episodes;
+                    if (L->eval_left == 0) L->mode = RLO_MODE_TRAIN;
+                }
+                if (L->mode == RLO_MODE_TRAIN && b->target_episodes && L->train_ep >= b->target_episodes)
+                    L->mode = RLO_MODE_DONE;
+            } else {
+                b->stats[3]++;
+                if (--L->eval_left == 0) {
+                    int fin = b->eval_only || (b->target_episodes && L->train_ep >= b->target_episodes);
+                    L->mode = fin ? RLO_MODE_DONE : RLO_MODE_TRAIN;
+                }
+            }
+        }
+    }
+    if (b->priv) return;
+    for (size_t k = 0; k < nq; ++k) {
+        b->q_g[k] = wrap_add(b->q_g[k], b->dq[k]);
+        b->f_g[k] |= b->df[k];
+    }
+}
+
+static void run_launch(rlo_batch *b) {
+    size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
+    memset(b->acc_q, 0, nq * 8); memset(b->acc_f, 0, nq); memset(b->acc_n, 0, nsa * 8);
+    b->acc_t = 0;
+    rlo_record *tmp = b->record ? (rlo_record *)malloc(sizeof(rlo_record) * b->G) : NULL;
+    size_t rec0 = b->records.n;
+    if (b->record) {
+        /* reserve [K][n_lanes] records */
+        rlo_record z;
+        memset(&z, 0, sizeof z);
+        for (size_t i = 0; i < (size_t)b->K * b->c.n_lanes; ++i) vpush(&b->records, &z);
+    }
+    if (b->priv) {
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+            lane_t *L = &b->lanes[i];
+            b->qd_g = L->qd; b->n_g = L->n; b->t_g = L->t;
+            for (uint32_t k = 0; k < b->K; ++k) {
+                group_step(b, i, 1, tmp);
+                if (tmp) ((rlo_record *)b->records.p)[rec0 + (size_t)k * b->c.n_lanes + i] = tmp[0];
+            }
+            L->t = b->t_g;
+        }
+        b->n_g = b->n_g_own;
+        b->stats[6]++;
+        free(tmp);
+        return;
+    }
+    for (uint32_t g = 0; g < b->n_groups; ++g) {
+        uint32_t lane0 = g * b->G;
+        uint32_t nl = b->c.n_lanes - lane0 < b->G ? b->c.n_lanes - lane0 : b->G;
+        memcpy(b->q_g, b->q_base, nq * 8); memcpy(b->f_g, b->f_base, nq);
+        memcpy(b->n_g, b->n_base, nsa * 4); b->t_g = b->t_base;
+        for (uint32_t k = 0; k < b->K; ++k) {
+            group_step(b, lane0, nl, tmp);
+            if (tmp) {
+                rlo_record *dst = (rlo_record *)b->records.p + rec0 + (size_t)k * b->c.n_lanes + lane0;
+                memcpy(dst, tmp, sizeof(rlo_record) * nl);
+            }
+        }
+        for (size_t i = 0; i < nq; ++i) {
+            b->acc_q[i] = wrap_add(b->acc_q[i], (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]));
+            b->acc_f[i] |= b->f_g[i];
+        }
+        for (size_t i = 0; i < nsa; ++i) b->acc_n[i] += (int64_t)b->n_g[i] - (int64_t)b->n_base[i];
+        b->acc_t += (int64_t)(b->t_g - b->t_base);
+    }
+    for (size_t i = 0; i < nq; ++i) {
+        b->q_base[i] = wrap_add(b->q_base[i], b->acc_q[i]);
+        b->f_base[i] |= b->acc_f[i];
+    }
+    for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + b->acc_n[i]);
+    b->t_base = (uint64_t)((int64_t)b->t_base + b->acc_t);
+    b->stats[6]++;
+    free(tmp);
+}
+
+void rlo_batch_run(rlo_batch *b, uint32_t n_launches) {
+    for (uint32_t i = 0; i < n_launches; ++i) run_launch(b);
+}
+static int all_done(const rlo_batch *b) {
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i)
+        if (b->lanes[i].mode != RLO_MODE_DONE) return 0;
+    return 1;
+}
+uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n, uint64_t eval_at) {
+    b->target_episodes = n; b->eval_at = eval_at; b->eval_only = 0;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        lane_t *L = &b->lanes[i];
+        L->need_reset = 1; L->train_ep = 0; L->eval_left = 0;
+        L->mode = n ? RLO_MODE_TRAIN : RLO_MODE_DONE;
+        if (L->trace) { memset(L->trace, 0, sizeof(double) * b->S * b->A); memset(L->visited, 0, b->S); }
+    }
+    uint64_t launches = 0;
+    while (!all_done(b)) { run_launch(b); launches++; }
+    b->target_episodes = 0; b->eval_at = 0;
+    return launches;
+}
+uint64_t rlo_batch_evaluate(rlo_batch *b, uint64_t n) {
+    b->eval_only = 1; b->target_episodes = 0; b->eval_at = 0;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        lane_t *L = &b->lanes[i];
+        L->need_reset = 1; L->eval_left = n;
+        L->mode = n ? RLO_MODE_EVAL : RLO_MODE_DONE;
+    }
+    uint64_t launches = 0;
+    while (!all_done(b)) { run_launch(b); launches++; }
+    b->eval_only = 0;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) b->lanes[i].mode = RLO_MODE_TRAIN;
+    return launches;
+}
+void rlo_batch_get_q(const rlo_batch *b, double *out) {
+    size_t nq = (size_t)b->P * b->S * b->A;
+    if (b->priv) {        /* [L][P][S][A] */
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(out + i * nq, b->lanes[i].qd, nq * sizeof(double));
+        return;
+    }
+    for (size_t i = 0; i < nq; ++i) out[i] = q_val(b->q_base[i], b->f_base[i]);
+}
+void rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out) {
+    memcpy(out, b->q_base, sizeof(int64_t) * b->P * b->S * b->A);
+}
+void rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out) {
+    memcpy(out, b->f_base, (size_t)b->P * b->S * b->A);
+}
+void rlo_batch_get_ucb(const rlo_batch *b, uint32_t *counts, uint64_t *t) {
+    if (b->priv) {        /* [L][S][A], t[L] */
+        size_t nsa = (size_t)b->S * b->A;
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+            memcpy(counts + i * nsa, b->lanes[i].n, nsa * sizeof(uint32_t));
+            t[i] = b->lanes[i].t;
+        }
+        return;
+    }
+    memcpy(counts, b->n_base, sizeof(uint32_t) * b->S * b->A);
+    *t = b->t_base;
+}
+uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap) {
+    uint64_t n = b->records.n;
+    if (out) memcpy(out, b->records.p, (n < cap ? n : cap) * sizeof(rlo_record));
+    b->records.n = 0;
+    return n;
+}
+uint64_t rlo_batch_n_records(const rlo_batch *b) { return b->records.n; }
+void rlo_batch_stats(const rlo_batch *b, uint64_t *out8) {
+    memcpy(out8, b->stats, sizeof b->stats);
+    uint64_t done = 0;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) done += b->lanes[i].mode == RLO_MODE_DONE;
+    out8[5] = done;
+}
+void rlo_batch_lane_eps(const rlo_batch *b, double *out) {
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) out[i] = b->lanes[i].eps;
+}

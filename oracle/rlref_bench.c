@@ -1,0 +1,69 @@
+/*
+ * rlref_bench.c — CPU baseline timer (test/bench infrastructure only).
+ *
+ * Times the faithful single-env restatement of the reference training loop
+ * (src/agent.rs:66-118 with src/agent/one_step_agent.rs:53-86, eval interleave
+ * on) on host cores: `threads` independent env+agent pairs, one per thread,
+ * no sharing — the reference itself is single-threaded.
+ *
+ * usage: rlref_bench <env> <map8x8> <slippery> <agent> <policy> <selector> <algo>
+ *                    <n_episodes> <eval_at> <threads>
+ * prints one JSON line: {"steps":..,"seconds":..,"threads":..,"steps_per_sec":..}
+ */
+#include "rlref.h"
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
+
+typedef struct {
+    rlo_config c;
+    uint64_t n_episodes, eval_at, steps;
+    double seconds;
+} job;
+
+static void *run(void *p) {
+    job *j = (job *)p;
+    j->steps = rlo_faithful_bench(&j->c, j->n_episodes, j->eval_at, &j->seconds);
+    return NULL;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 11) {
+        fprintf(stderr, "usage: %s env map8x8 slippery agent policy selector algo n_episodes eval_at threads\n",
+                argv[0]);
+        return 2;
+    }
+    rlo_config c = {0};
+    c.env = atoi(argv[1]); c.map8x8 = atoi(argv[2]); c.slippery = atoi(argv[3]);
+    c.agent = atoi(argv[4]); c.policy = atoi(argv[5]); c.selector = atoi(argv[6]); c.algo = atoi(argv[7]);
+    uint64_t n = strtoull(argv[8], NULL, 10), eval_at = strtoull(argv[9], NULL, 10);
+    int threads = atoi(argv[10]);
+    if (threads < 1) threads = 1;
+    /* CLI defaults of the reference bins: src/bin/frozen_lake.rs:35-73,84 */
+    c.max_steps = 100; c.lr = 0.05; c.gamma = 0.95; c.lambda_ = 0.5; c.eps0 = 1.0;
+    c.eps_decay = 1.0 / (0.5 * (double)n); c.eps_final = 0.0; c.ucb_c = 0.5; c.q_default = 0.0;
+    c.seed = 0x5EED; c.n_lanes = 1; c.group_size = 1; c.sync_every = 1; c.eval_episodes = 100;
+    job *jobs = (job *)calloc((size_t)threads, sizeof(job));
+    pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; ++i) {
+        jobs[i].c = c;
+        jobs[i].c.lane_offset = (uint64_t)i;
+        jobs[i].n_episodes = n;
+        jobs[i].eval_at = eval_at;
+        pthread_create(&tid[i], NULL, run, &jobs[i]);
+    }
+    uint64_t steps = 0;
+    for (int i = 0; i < threads; ++i) {
+        pthread_join(tid[i], NULL);
+        steps += jobs[i].steps;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    double sec = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    printf("{\"steps\": %llu, \"seconds\": %.6f, \"threads\": %d, \"steps_per_sec\": %.3f}\n",
+           (unsigned long long)steps, sec, threads, (double)steps / sec);
+    free(jobs); free(tid);
+    return 0;
+}

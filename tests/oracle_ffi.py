@@ -1,0 +1,318 @@
+"""ctypes binding to the CPU oracle (oracle/_build/librlref.so).
+
+TEST INFRASTRUCTURE ONLY: the oracle is the checker, never the product path.
+See oracle/rlref.h for what it restates and its parity status.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "_build", "librlref.so")
+
+ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}
+AGENT = {"one_step": 0, "traces": 1}
+POLICY = {"tabular": 0, "double": 1}
+SELECTOR = {"eps_greedy": 0, "ucb": 1}
+ALGO = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}
+MODE_TRAIN, MODE_EVAL, MODE_DONE = 0, 1, 2
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("env", C.c_int32), ("map8x8", C.c_int32), ("slippery", C.c_int32),
+        ("max_steps", C.c_uint32),
+        ("agent", C.c_int32), ("policy", C.c_int32), ("selector", C.c_int32),
+        ("algo", C.c_int32), ("decay_kind", C.c_int32),
+        ("lr", C.c_double), ("gamma", C.c_double), ("lambda_", C.c_double),
+        ("eps0", C.c_double), ("eps_decay", C.c_double), ("eps_final", C.c_double),
+        ("ucb_c", C.c_double), ("q_default", C.c_double),
+        ("seed", C.c_uint64), ("lane_offset", C.c_uint64),
+        ("n_lanes", C.c_uint32), ("group_size", C.c_uint32), ("sync_every", C.c_uint32),
+        ("eval_episodes", C.c_uint32),
+    ]
+
+
+RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
+                         ("term", "u1"), ("mode", "u1"), ("pad", "<u4"),
+                         ("r", "<f8"), ("td", "<f8")])
+assert RECORD_DTYPE.itemsize == 32
+
+
+def default_params(**kw):
+    """Reference CLI defaults (src/bin/frozen_lake.rs:35-73, decay :84)."""
+    p = dict(env="frozen_lake", map8x8=0, slippery=0, max_steps=100, agent="one_step",
+             policy="tabular", selector="eps_greedy", algo="qlearning", decay_kind=0,
+             lr=0.05, gamma=0.95, lambda_=0.5, eps0=1.0, n_episodes_for_decay=100000,
+             exploration_time=0.5, eps_final=0.0, ucb_c=0.5, q_default=0.0, seed=0x5EED,
+             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100)
+    p.update(kw)
+    if "eps_decay" not in p:
+        p["eps_decay"] = p["eps0"] / (p["exploration_time"] * p["n_episodes_for_decay"])
+    return p
+
+
+def make_config(p):
+    c = Config()
+    c.env = ENV[p["env"]] if isinstance(p["env"], str) else p["env"]
+    c.map8x8, c.slippery, c.max_steps = p["map8x8"], p["slippery"], p["max_steps"]
+    c.agent = AGENT[p["agent"]] if isinstance(p["agent"], str) else p["agent"]
+    c.policy = POLICY[p["policy"]] if isinstance(p["policy"], str) else p["policy"]
+    c.selector = SELECTOR[p["selector"]] if isinstance(p["selector"], str) else p["selector"]
+    c.algo = ALGO[p["algo"]] if isinstance(p["algo"], str) else p["algo"]
+    c.decay_kind = p["decay_kind"]
+    for k in ("lr", "gamma", "lambda_", "eps0", "eps_decay", "eps_final", "ucb_c", "q_default"):
+        setattr(c, k, float(p[k]))
+    c.seed, c.lane_offset = p["seed"], p["lane_offset"]
+    c.n_lanes, c.group_size, c.sync_every = p["n_lanes"], p["group_size"], p["sync_every"]
+    c.eval_episodes = p["eval_episodes"]
+    return c
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.rlo_log.restype = C.c_double
+        L.rlo_log.argtypes = [C.c_double]
+        L.rlo_rng_stream.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, P(C.c_uint32)]
+        L.rlo_u64_to_uniform01.restype = C.c_double
+        L.rlo_u64_to_uniform01.argtypes = [C.c_uint64]
+        L.rlo_uniform_int_u64.restype = C.c_uint32
+        L.rlo_uniform_int_u64.argtypes = [C.c_uint64, C.c_uint64, P(C.c_int)]
+        L.rlo_uniform_card_u32.restype = C.c_uint32
+        L.rlo_uniform_card_u32.argtypes = [C.c_uint32, P(C.c_int)]
+        L.rlo_blackjack_obs_id.restype = C.c_uint64
+        L.rlo_blackjack_obs_id.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.rlo_env_dims.argtypes = [P(Config), P(C.c_uint32), P(C.c_uint32)]
+        L.rlo_env_table.argtypes = [P(Config), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rlo_env_start.argtypes = [P(Config), C.c_void_p]
+        L.rlo_faithful_create.restype = C.c_void_p
+        L.rlo_faithful_create.argtypes = [P(Config)]
+        L.rlo_faithful_destroy.argtypes = [C.c_void_p]
+        L.rlo_faithful_train.restype = C.c_uint64
+        L.rlo_faithful_train.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.rlo_faithful_evaluate.restype = C.c_uint64
+        L.rlo_faithful_evaluate.argtypes = [C.c_void_p, C.c_uint64]
+        L.rlo_faithful_reset.argtypes = [C.c_void_p]
+        L.rlo_faithful_get_q.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_faithful_n_episodes.restype = C.c_uint64
+        L.rlo_faithful_n_episodes.argtypes = [C.c_void_p]
+        L.rlo_faithful_n_steps.restype = C.c_uint64
+        L.rlo_faithful_n_steps.argtypes = [C.c_void_p]
+        L.rlo_faithful_histories.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rlo_faithful_get_records.restype = C.c_uint64
+        L.rlo_faithful_get_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.rlo_faithful_set_record.argtypes = [C.c_void_p, C.c_int]
+        L.rlo_faithful_epsilon.restype = C.c_double
+        L.rlo_faithful_epsilon.argtypes = [C.c_void_p]
+        L.rlo_batch_create.restype = C.c_void_p
+        L.rlo_batch_create.argtypes = [P(Config)]
+        L.rlo_batch_destroy.argtypes = [C.c_void_p]
+        L.rlo_batch_run.argtypes = [C.c_void_p, C.c_uint32]
+        L.rlo_batch_train_episodes.restype = C.c_uint64
+        L.rlo_batch_train_episodes.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.rlo_batch_evaluate.restype = C.c_uint64
+        L.rlo_batch_evaluate.argtypes = [C.c_void_p, C.c_uint64]
+        L.rlo_batch_reset.argtypes = [C.c_void_p]
+        L.rlo_batch_get_q.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_get_q_raw.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_get_qflags.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_get_ucb.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rlo_batch_set_record.argtypes = [C.c_void_p, C.c_int]
+        L.rlo_batch_take_records.restype = C.c_uint64
+        L.rlo_batch_take_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.rlo_batch_n_records.restype = C.c_uint64
+        L.rlo_batch_n_records.argtypes = [C.c_void_p]
+        L.rlo_batch_stats.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_lane_eps.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_set_selector.argtypes = [C.c_void_p, C.c_int32]
+        L.rlo_batch_set_algo.argtypes = [C.c_void_p, C.c_int32]
+        _lib = L
+    return _lib
+
+
+def dims(p):
+    c = make_config(p)
+    S, A = C.c_uint32(), C.c_uint32()
+    assert lib().rlo_env_dims(C.byref(c), C.byref(S), C.byref(A)) == 0
+    return S.value, A.value
+
+
+def env_table(p):
+    S, A = dims(p)
+    c = make_config(p)
+    n = S * A * 3
+    prob = np.zeros(n, np.float64)
+    nxt = np.zeros(n, np.uint32)
+    rew = np.zeros(n, np.float64)
+    term = np.zeros(n, np.uint8)
+    rc = lib().rlo_env_table(C.byref(c), prob.ctypes.data, nxt.ctypes.data, rew.ctypes.data,
+                             term.ctypes.data)
+    assert rc == 0
+    start = np.zeros(S, np.float64)
+    assert lib().rlo_env_start(C.byref(c), start.ctypes.data) == 0
+    shp = (S, A, 3)
+    return dict(prob=prob.reshape(shp), next=nxt.reshape(shp), reward=rew.reshape(shp),
+                term=term.reshape(shp), start=start)
+
+
+def rng_stream(seed, lane, n):
+    out = np.zeros(n, np.uint32)
+    lib().rlo_rng_stream(seed, lane, n, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+class Faithful:
+    """Single env + agent, f64 Q: src/agent.rs:66-141 restated."""
+
+    def __init__(self, p):
+        self.p = p
+        self.S, self.A = dims(p)
+        self.P = 2 if p["policy"] == "double" else 1
+        self.cfg = make_config(p)
+        self.h = lib().rlo_faithful_create(C.byref(self.cfg))
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rlo_faithful_destroy(self.h)
+            self.h = None
+
+    def set_record(self, on=True):
+        lib().rlo_faithful_set_record(self.h, int(on))
+
+    def train(self, n_episodes, eval_at=0):
+        return lib().rlo_faithful_train(self.h, n_episodes, eval_at)
+
+    def evaluate(self, n_episodes):
+        return lib().rlo_faithful_evaluate(self.h, n_episodes)
+
+    def reset(self):
+        lib().rlo_faithful_reset(self.h)
+
+    def q(self):
+        out = np.zeros(self.P * self.S * self.A, np.float64)
+        lib().rlo_faithful_get_q(self.h, out.ctypes.data)
+        return out.reshape(self.P, self.S, self.A)
+
+    def histories(self):
+        ne = lib().rlo_faithful_n_episodes(self.h)
+        ns = lib().rlo_faithful_n_steps(self.h)
+        rh = np.zeros(ne, np.float64)
+        el = np.zeros(ne, np.uint64)
+        te = np.zeros(ns, np.float64)
+        lib().rlo_faithful_histories(self.h, rh.ctypes.data, el.ctypes.data, te.ctypes.data)
+        return rh, el, te
+
+    def records(self):
+        n = lib().rlo_faithful_get_records(self.h, None, 0)
+        out = np.zeros(n, RECORD_DTYPE)
+        lib().rlo_faithful_get_records(self.h, out.ctypes.data, n)
+        return out
+
+    def epsilon(self):
+        return lib().rlo_faithful_epsilon(self.h)
+
+
+class Batch:
+    """The batched schedule the GPU implements (fixed-point Q)."""
+
+    def __init__(self, p):
+        self.p = p
+        self.S, self.A = dims(p)
+        self.P = 2 if p["policy"] == "double" else 1
+        self.L = p["n_lanes"]
+        self.cfg = make_config(p)
+        self.h = lib().rlo_batch_create(C.byref(self.cfg))
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rlo_batch_destroy(self.h)
+            self.h = None
+
+    def set_record(self, on=True):
+        lib().rlo_batch_set_record(self.h, int(on))
+
+    def run(self, n_launches):
+        lib().rlo_batch_run(self.h, n_launches)
+
+    def train_episodes(self, n, eval_at=0):
+        return lib().rlo_batch_train_episodes(self.h, n, eval_at)
+
+    def evaluate(self, n):
+        return lib().rlo_batch_evaluate(self.h, n)
+
+    def reset(self):
+        lib().rlo_batch_reset(self.h)
+
+    def set_selector(self, s):
+        lib().rlo_batch_set_selector(self.h, SELECTOR[s])
+
+    def set_algo(self, a):
+        lib().rlo_batch_set_algo(self.h, ALGO[a])
+
+    @property
+    def private(self):
+        return self.p["group_size"] == 1
+
+    def q(self):
+        """shared mode: [P,S,A]; private mode (G == 1): [L,P,S,A]"""
+        n = self.P * self.S * self.A * (self.L if self.private else 1)
+        out = np.zeros(n, np.float64)
+        lib().rlo_batch_get_q(self.h, out.ctypes.data)
+        if self.private:
+            return out.reshape(self.L, self.P, self.S, self.A)
+        return out.reshape(self.P, self.S, self.A)
+
+    def q_raw(self):
+        out = np.zeros(self.P * self.S * self.A, np.int64)
+        lib().rlo_batch_get_q_raw(self.h, out.ctypes.data)
+        return out.reshape(self.P, self.S, self.A)
+
+    def qflags(self):
+        out = np.zeros(self.P * self.S * self.A, np.uint8)
+        lib().rlo_batch_get_qflags(self.h, out.ctypes.data)
+        return out.reshape(self.P, self.S, self.A)
+
+    def ucb(self):
+        if self.private:
+            n = np.zeros(self.L * self.S * self.A, np.uint32)
+            t = np.zeros(self.L, np.uint64)
+            lib().rlo_batch_get_ucb(self.h, n.ctypes.data, t.ctypes.data)
+            return n.reshape(self.L, self.S, self.A), t
+        n = np.zeros(self.S * self.A, np.uint32)
+        t = C.c_uint64()
+        lib().rlo_batch_get_ucb(self.h, n.ctypes.data, C.byref(t))
+        return n.reshape(self.S, self.A), t.value
+
+    def records(self):
+        """[n_steps, n_lanes] records since the last call (clears the buffer)."""
+        n = lib().rlo_batch_n_records(self.h)
+        out = np.zeros(n, RECORD_DTYPE)
+        lib().rlo_batch_take_records(self.h, out.ctypes.data, n)
+        return out.reshape(-1, self.L)
+
+    def stats(self):
+        out = np.zeros(8, np.uint64)
+        lib().rlo_batch_stats(self.h, out.ctypes.data)
+        return out
+
+    def lane_eps(self):
+        out = np.zeros(self.L, np.float64)
+        lib().rlo_batch_lane_eps(self.h, out.ctypes.data)
+        return out
