@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""bench.py — training env-steps/s of the MI355X hot path.
+
+Workload (BASELINE.json configs[1]): FrozenLake-8x8 (deterministic), one-step
+Q-learning, eps-greedy, 2^20 lanes per GPU, learner groups of 256 lanes
+(one workgroup, Q in LDS), merge every K=64 synchronous steps.
+One bench "step" = one launch = K synchronous env-steps of every lane + the
+merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel
+(k_train_shared) against HBM with SURVEY §8(d)'s 32 B/env-step; `cpu_baseline`
+times the oracle's faithful single-env restatement of the reference loop on
+one host core (bounded sample).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rl-rust_amd"))
+
+METRIC = "env-steps/sec, FrozenLake-8x8 Q-learning, 2^20 envs, 1/2/4/8 GPUs"
+BYTES_PER_STEP = 32          # 16-B lane record read + written per env-step
+HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--lanes", type=int, default=1 << 20, help="env lanes per GPU")
+    ap.add_argument("--group", type=int, default=256)
+    ap.add_argument("--sync", type=int, default=64, help="K: synchronous steps per launch")
+    ap.add_argument("--env", default="frozen_lake")
+    ap.add_argument("--map8x8", type=int, default=1)
+    ap.add_argument("--slippery", type=int, default=0)
+    ap.add_argument("--agent", default="one_step")
+    ap.add_argument("--policy", default="tabular")
+    ap.add_argument("--selector", default="eps_greedy")
+    ap.add_argument("--algo", default="qlearning")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Faithful single-env restatement of the reference loop (oracle, 1 core),
+    FrozenLake-8x8 Q-learning eps-greedy, no eval interleave; sample sized to
+    ~cpu_seconds of work."""
+    exe = os.path.join(ROOT, "oracle", "_build", "rlref_bench")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    envk = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}[args.env]
+    agentk = {"one_step": 0, "traces": 1}[args.agent]
+    polk = {"tabular": 0, "double": 1}[args.policy]
+    selk = {"eps_greedy": 0, "ucb": 1}[args.selector]
+    algok = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}[args.algo]
+
+    def run(n):
+        out = subprocess.run([exe, str(envk), str(args.map8x8), str(args.slippery), str(agentk),
+                              str(polk), str(selk), str(algok), str(n), "0", "1"],
+                             check=True, capture_output=True, text=True).stdout
+        return json.loads(out)
+
+    probe = run(20000)
+    rate = probe["steps"] / max(probe["seconds"], 1e-6)
+    eps_per_sec = 20000 / max(probe["seconds"], 1e-6)
+    n = max(20000, int(eps_per_sec * args.cpu_seconds))
+    r = run(n)
+    return {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle faithful single-env loop (src/agent.rs:66-118 restated in C), "
+                      f"{args.env} {'8x8' if args.map8x8 else '4x4'} {args.agent} {args.algo} "
+                      f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s "
+                      f"(probe {rate:.3g} steps/s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # loaded before librlamd so both share one HIP runtime
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import rlamd
+
+    p = rlamd.default_params(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
+                             agent=args.agent, policy=args.policy, selector=args.selector,
+                             algo=args.algo, n_lanes=args.lanes, group_size=args.group,
+                             sync_every=args.sync, lane_offset=rank * args.lanes,
+                             device=local_rank)
+    agent = rlamd.Agent(p)
+    stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
+    torch.cuda.set_stream(stream)
+    agent.set_stream(stream.cuda_stream)
+    delta = None
+    if world > 1:
+        delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{local_rank}")
+        agent.set_delta_buffer(delta.data_ptr(), delta.numel())
+
+    def step():
+        agent.launch_train()
+        if delta is not None:
+            dist.all_reduce(delta)          # ΔQ / ΔN / Δt: exact int64 sum over ranks (RCCL)
+        agent.launch_apply()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    st0 = agent.stats()
+    agent.set_timing(True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms, n_kern = agent.timing()
+    st1 = agent.stats()
+    steps_done = st1["train_steps"] - st0["train_steps"]
+    expect = args.steps * args.sync * args.lanes
+    assert steps_done == expect, (steps_done, expect)
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_steps = world * expect
+    value = total_steps / wall
+    avg_kern_s = kern_ms / max(n_kern, 1) / 1e3
+    bytes_per_launch = BYTES_PER_STEP * args.lanes * args.sync
+    achieved = bytes_per_launch / avg_kern_s
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tf = json.load(open(args.traffic_file))
+            if tf.get("lanes") == args.lanes and tf.get("sync") == args.sync and tf.get("env") == args.env:
+                traffic = tf.get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+    out = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (env lanes seeded per global lane id; no dataset)",
+        "config": {"workload": f"{args.env} {'8x8' if args.map8x8 else '4x4'}"
+                               f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
+                               f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
+                   "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
+                   "env_steps_per_launch": args.lanes * args.sync, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                     "traffic": traffic,
+                     "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
+                     "kernel_launches": n_kern,
+                     "bytes_per_launch": bytes_per_launch},
+        "torch_event_ms": ev0.elapsed_time(ev1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    agent.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+/*
+ * rl.h — C ABI of librlamd.so, the MI355X-native (gfx950, HIP) tabular-RL hot path.
+ *
+ * This is the drop-in boundary for JohnVithor/RL-Rust's per-step training loop
+ * (reference: /root/reference, cited path:line).  The reference has no FFI;
+ * its interfaces are Rust traits:
+ *   Env<T,COUNT>            src/env.rs:19-49
+ *   Agent<T,COUNT>          src/agent.rs:47-164
+ *   Policy<T,COUNT>         src/policy.rs:15-33          (EnumPolicy)
+ *   ActionSelection<T,COUNT> src/action_selection.rs:10-22 (EnumActionSelection)
+ *   GetNextQValue fn ptr    src/agent.rs:17  (sarsa / qlearning / expected_sarsa)
+ * Each export below names the trait method it replaces.  Closures and fn
+ * pointers become enums; every Env/Agent is BATCHED over `n_lanes` lanes
+ * (lane = one env instance + its RNG stream).  The Rust binding a maintainer
+ * would add is shown in INTEGRATION.md.
+ *
+ * Ownership: a handle owns all its device memory; host buffers passed in are
+ * owned by the caller and only read/written during the call.  Sizes are
+ * explicit.  No callbacks, no C++ exceptions cross this boundary.  One handle
+ * per host thread (not thread-safe), like the reference's !Send agents.
+ * Errors: every int-returning call returns RL_OK or an RL_E_* code; the
+ * message is in rl_last_error().  EnvNotReady (src/env.rs:17) is RL_E_NOT_READY.
+ */
+#ifndef RL_AMD_RL_H
+#define RL_AMD_RL_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_ABI_VERSION 1
+
+enum rl_status {
+    RL_OK = 0,
+    RL_E_NOT_READY = 1, /* Env::step on a terminated/unreset env (src/env.rs:16-17,24) */
+    RL_E_ARG = 2,       /* invalid argument / size */
+    RL_E_HIP = 3,       /* HIP runtime failure */
+    RL_E_OOM = 4,       /* device allocation failed */
+    RL_E_STATE = 5      /* call not valid in the handle's current mode */
+};
+
+enum rl_env_kind {      /* src/env/{frozen_lake,cliff_walking,taxi,blackjack}.rs */
+    RL_ENV_FROZEN_LAKE = 0, RL_ENV_CLIFF_WALKING = 1, RL_ENV_TAXI = 2, RL_ENV_BLACKJACK = 3
+};
+enum rl_agent_kind {    /* src/agent/one_step_agent.rs, src/agent/elegibility_traces_agent.rs */
+    RL_AGENT_ONE_STEP = 0, RL_AGENT_TRACES = 1
+};
+enum rl_policy_kind {   /* src/policy/tabular_policy.rs, src/policy/double_tabular_policy.rs */
+    RL_POLICY_TABULAR = 0, RL_POLICY_DOUBLE = 1
+};
+enum rl_selector_kind { /* src/action_selection/{uniform_epsilon_greed,upper_confidence_bound}.rs */
+    RL_SEL_EPS_GREEDY = 0, RL_SEL_UCB = 1
+};
+enum rl_algo_kind {     /* src/agent.rs:19-45 sarsa / qlearning / expected_sarsa */
+    RL_ALGO_SARSA = 0, RL_ALGO_QLEARNING = 1, RL_ALGO_EXPECTED_SARSA = 2
+};
+enum rl_decay_kind {    /* the epsilon_decay closure: `a - d` (src/bin/frozen_lake.rs:146) or `a * d`
+                           (src/bin/frozen_lake_neural.rs:181) */
+    RL_DECAY_LINEAR = 0, RL_DECAY_MUL = 1
+};
+enum rl_lane_mode { RL_MODE_TRAIN = 0, RL_MODE_EVAL = 1, RL_MODE_DONE = 2 };
+
+/* Env constructor arguments: FrozenLakeEnv::new(map, is_slippery, max_steps)
+ * (src/env/frozen_lake.rs:48), CliffWalkingEnv::new(max_steps) (cliff_walking.rs:34),
+ * TaxiEnv::new(max_steps) (taxi.rs:57), BlackJackEnv::new() (blackjack.rs:32). */
+typedef struct rl_env_config {
+    int32_t kind;       /* rl_env_kind */
+    int32_t map8x8;     /* FrozenLake: 0 = MAP_4X4, 1 = MAP_8X8 (frozen_lake.rs:23-28) */
+    int32_t slippery;   /* FrozenLake --stochastic_env */
+    uint32_t max_steps; /* truncation (frozen_lake.rs:119); ignored by Blackjack */
+} rl_env_config;
+
+/* Agent constructor arguments, gathered from the bins (src/bin/frozen_lake.rs:140-165):
+ * OneStepAgent::new / ElegibilityTracesAgent::new + TabularPolicy::new(lr, default)
+ * + UniformEpsilonGreed::new(eps0, decay, final) | UpperConfidenceBound::new(c). */
+typedef struct rl_agent_config {
+    rl_env_config env;
+    int32_t agent, policy, selector, algo, decay_kind;
+    double lr, gamma, lambda, eps0, eps_decay, eps_final, ucb_c, q_default;
+    uint64_t seed;        /* per-lane RNG key (replaces thread_rng) */
+    uint64_t lane_offset; /* global id of local lane 0 (multi-GPU sharding) */
+    uint32_t n_lanes;     /* env instances on this device */
+    uint32_t group_size;  /* lanes sharing one Q copy; 1 = private f64 agents (bit-exact reference) */
+    uint32_t sync_every;  /* K: synchronous steps per launch; groups merge after every launch */
+    uint32_t eval_episodes; /* episodes per in-train evaluate() (src/agent.rs:108 uses 100) */
+    int32_t device;       /* HIP device ordinal */
+} rl_agent_config;
+
+/* One per lane per synchronous step (recording mode only): the integer stream
+ * (s, a, r, terminated, s', a') plus the TD error pushed to training_error
+ * (src/agent.rs:98).  For Blackjack s/s2 are dense indices (see rl_blackjack_obs_id). */
+typedef struct rl_step_record {
+    uint32_t s, s2;
+    uint8_t a, a2, term, mode;
+    uint32_t pad;
+    double r, td;
+} rl_step_record;
+
+/* Counters accumulated since rl_agent_create / rl_agent_reset_stats. */
+typedef struct rl_stats {
+    uint64_t train_steps;     /* every Env::step inside train, truncation step included */
+    uint64_t eval_steps;      /* steps of in-train evaluate() episodes (excluded from the metric) */
+    uint64_t train_episodes;
+    uint64_t eval_episodes;
+    int64_t reward_sum_q16;   /* sum of training-episode rewards, fixed point 2^-16 */
+    uint64_t done_lanes;      /* lanes that finished the current train()/evaluate() call */
+    uint64_t launches;
+    uint64_t reserved;
+} rl_stats;
+
+typedef struct rl_env rl_env;
+typedef struct rl_agent rl_agent;
+
+/* ---------------------------------------------------------------- misc */
+const char *rl_last_error(void);
+int rl_abi_version(void);
+int rl_device_count(int *count);
+/* usize observation id of the reference's Blackjack env: fxhash 0.2.1 of
+ * BlackJackObservation{p_score,d_score,p_ace} (src/env/blackjack.rs:25-27). */
+uint64_t rl_blackjack_obs_id(uint32_t p_score, uint32_t d_score, uint32_t p_ace);
+/* dense state index <-> reference observation (Blackjack: fxhash id; others: identity) */
+uint64_t rl_obs_to_reference(int32_t env_kind, uint32_t dense_state);
+/* |S| and COUNT (Env::action_size, src/env.rs:20-22) for an env config */
+int rl_env_dims(const rl_env_config *cfg, uint32_t *n_states, uint32_t *n_actions);
+/* Host-side export of the packed device transition tables, decoded to the
+ * reference's layout probs[s][a][3] = (p, s', r, term) (frozen_lake.rs:56,
+ * cliff_walking.rs:12, taxi.rs:14) plus the initial-state distribution.
+ * Needs no GPU.  Not available for Blackjack (no table). */
+int rl_env_table(const rl_env_config *cfg, double *prob, uint32_t *next, double *reward,
+                 uint8_t *term, double *start);
+
+/* ---------------------------------------------------------------- Env (batched) */
+/* Env::new for n_envs lanes; lane i draws from stream (seed, lane_offset + i). */
+int rl_env_create(const rl_env_config *cfg, uint32_t n_envs, uint64_t seed, uint64_t lane_offset,
+                  int32_t device, rl_env **out);
+void rl_env_destroy(rl_env *env);
+/* Env::reset (src/env.rs:23) for every lane: obs_out[n_envs] (usize observations) */
+int rl_env_reset(rl_env *env, uint64_t *obs_out);
+/* Env::step (src/env.rs:24) for every lane.  Returns RL_E_NOT_READY (and steps
+ * no lane) if any lane is not ready — the batched Err(EnvNotReady). */
+int rl_env_step(rl_env *env, const uint32_t *actions, uint64_t *obs_out, double *reward_out,
+                uint8_t *terminated_out);
+
+/* ---------------------------------------------------------------- Agent (batched) */
+int rl_agent_create(const rl_agent_config *cfg, rl_agent **out);
+void rl_agent_destroy(rl_agent *a);
+/* Agent::set_future_q_value_func (src/agent.rs:48) */
+int rl_agent_set_future_q_value_func(rl_agent *a, int32_t algo);
+/* Agent::set_action_selector (src/agent.rs:50) with a freshly constructed selector */
+int rl_agent_set_action_selector(rl_agent *a, int32_t selector, double eps0, double eps_decay,
+                                 double eps_final, int32_t decay_kind, double ucb_c);
+/* Agent::reset (one_step_agent.rs:43-46): policy to default, selector fresh */
+int rl_agent_reset(rl_agent *a);
+/* Agent::train(env, n_episodes, eval_at) (src/agent.rs:66-118) for every lane:
+ * returns when every lane has run n_episodes training episodes (eval_at = 0
+ * disables the evaluate() interleave; the reference panics on 0). */
+int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out);
+/* Agent::evaluate(env, n_episodes) (src/agent.rs:120-141) for every lane */
+int rl_agent_evaluate(rl_agent *a, uint64_t n_episodes, rl_stats *out);
+/* Throughput mode: enqueue n launches of K = sync_every synchronous steps over
+ * all lanes (lanes train forever, episodes restart), each followed by the group
+ * merge.  Asynchronous on the handle's stream. */
+int rl_agent_run(rl_agent *a, uint32_t n_launches);
+int rl_agent_synchronize(rl_agent *a);
+int rl_agent_stats(rl_agent *a, rl_stats *out);
+/* Policy::get_values for every (s,a): shared mode (group_size>1): [P][S][A]
+ * merged Q; private mode (group_size==1): [n_lanes][P][S][A].  P = 2 for the
+ * double policy (alpha, beta).  n = number of doubles in out. */
+int rl_agent_get_q(rl_agent *a, double *out, size_t n);
+int rl_agent_set_q(rl_agent *a, const double *in, size_t n);
+/* shared mode only: raw fixed-point Q (value = raw * 2^-40) */
+int rl_agent_get_q_raw(rl_agent *a, int64_t *out, size_t n);
+/* UCB counters (upper_confidence_bound.rs:11-12): shared [S][A] + t[1];
+ * private [n_lanes][S][A] + t[n_lanes] */
+int rl_agent_get_ucb(rl_agent *a, uint32_t *counts, size_t n_counts, uint64_t *t, size_t n_t);
+/* per-lane epsilon (UniformEpsilonGreed::epsilon, uniform_epsilon_greed.rs:13) */
+int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n);
+/* recording: every launch appends K*n_lanes rl_step_record ([step][lane]) */
+int rl_agent_set_recording(rl_agent *a, int32_t enable);
+int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64_t *n_total);
+int rl_agent_dims(rl_agent *a, uint32_t *n_states, uint32_t *n_actions, uint32_t *n_tables);
+/* raw per-lane records (4 x u32 each): core = {s, flags|a|mode, env word, train episodes},
+ * aux = {eps lo, eps hi, eval episodes left, episode length}; for checkpoints and tests */
+int rl_agent_lane_state(rl_agent *a, uint32_t *core, uint32_t *aux, size_t n_lanes);
+
+/* -------- multi-GPU: the ΔQ merge as an external collective (shared mode) */
+/* number of int64 words of the merge delta (ΔQ, ΔN, Δt, Δflags) */
+int rl_agent_delta_words(rl_agent *a, uint64_t *n);
+/* use caller-owned device memory (e.g. a torch int64 tensor, zeroed) as the delta */
+int rl_agent_set_delta_buffer(rl_agent *a, void *device_ptr, uint64_t n_words);
+/* one launch = train kernel (writes this device's ΔQ into the delta buffer) ... */
+int rl_agent_launch_train(rl_agent *a);
+/* ... [caller all-reduces the delta buffer across ranks] ... then Q_base += Δ, Δ = 0 */
+int rl_agent_launch_apply(rl_agent *a);
+/* run on a caller stream (hipStream_t as void*); NULL = the handle's own stream */
+int rl_agent_set_stream(rl_agent *a, void *stream);
+/* HIP-event timing of every train kernel launch */
+int rl_agent_set_timing(rl_agent *a, int32_t enable);
+int rl_agent_get_timing(rl_agent *a, double *total_ms, uint64_t *n_launches);
+
+/* -------- device known-answer probes (numerics parity; need a GPU) */
+int rl_kat_log(int32_t device, const double *x, double *out, uint32_t n);
+int rl_kat_rng(int32_t device, uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out);
+int rl_kat_ucb(int32_t device, const double *q, const double *n_count, const uint64_t *t,
+               double c, double *out, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

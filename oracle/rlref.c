@@ -363,7 +363,7 @@ static int build_env(envdef *E, const rlo_config *c) {
     case RLO_ENV_FROZEN_LAKE: build_frozen_lake(E, c->map8x8, c->slippery); return 0;
     case RLO_ENV_CLIFF_WALKING: build_cliff_walking(E); return 0;
     case RLO_ENV_TAXI: build_taxi(E); return 0;
-    case RLO_ENV_BLACKJACK: E->S = 32 * 32 * 2; E->A = 2; return 0;
+    case RLO_ENV_BLACKJACK: E->S = 32 * 27 * 2; E->A = 2; return 0;
     }
     return -1;
 }
@@ -393,7 +393,8 @@ int rlo_env_start(const rlo_config *c, double *start) {
 
 /* blackjack helpers: src/env/blackjack.rs:47-83 */
 static inline uint32_t bj_score(uint32_t sum, uint32_t ace) { return (ace && sum + 10 <= 21) ? sum + 10 : sum; }
-static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 32 + d) * 2 + (ace ? 1 : 0); }
+/* dense obs index: p_score <= 31, d_score <= 26 (dealer stops at >= 17) */
+static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 27 + d) * 2 + (ace ? 1 : 0); }
 static void bj_initialize_hands(envstate *st, rlo_rng *r) {       /* :47-56 */
     uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
     st->p_sum = p0 + p1; st->d_sum = d0 + d1; st->d0 = d0;
@@ -760,11 +761,12 @@ struct rlo_batch {
     uint64_t t_base;
     /* current group scratch */
     int64_t *q_g, *dq;
+    uint32_t *dc;        /* contributions per entry this step */
     uint8_t *f_g, *df;
     uint32_t *n_g, *n_g_own;
     uint64_t t_g;
     /* merge accumulators */
-    int64_t *acc_q; uint8_t *acc_f; int64_t *acc_n; int64_t acc_t;
+    int64_t *acc_q, *acc_c; uint8_t *acc_f; int64_t *acc_n; int64_t acc_t;
     lane_t *lanes;
     uint64_t target_episodes, eval_at;
     int eval_only;
@@ -850,7 +852,9 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
     b->q_base = (int64_t *)malloc(nq * 8); b->f_base = (uint8_t *)calloc(nq, 1);
     b->q_g = (int64_t *)malloc(nq * 8); b->f_g = (uint8_t *)calloc(nq, 1);
     b->dq = (int64_t *)calloc(nq, 8); b->df = (uint8_t *)calloc(nq, 1);
+    b->dc = (uint32_t *)calloc(nq, 4);
     b->acc_q = (int64_t *)calloc(nq, 8); b->acc_f = (uint8_t *)calloc(nq, 1);
+    b->acc_c = (int64_t *)calloc(nq, 8);
     b->n_base = (uint32_t *)calloc(nsa, 4); b->n_g = b->n_g_own = (uint32_t *)calloc(nsa, 4);
     b->acc_n = (int64_t *)calloc(nsa, 8);
     b->records.esz = sizeof(rlo_record);
@@ -875,7 +879,7 @@ void rlo_batch_destroy(rlo_batch *b) {
         free(b->lanes[i].trace); free(b->lanes[i].visited); free(b->lanes[i].qd); free(b->lanes[i].n);
     }
     free(b->lanes); free(b->q_base); free(b->f_base); free(b->q_g); free(b->f_g); free(b->dq);
-    free(b->df); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
+    free(b->df); free(b->dc); free(b->acc_c); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
     free(b->records.p);
     free(b);
 }
@@ -924,7 +928,18 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
     uint8_t fl = 0;
     int64_t d = q_fix(delta, &fl);
     b->dq[k] = wrap_add(b->dq[k], d);
+    b->dc[k] += 1;
     b->df[k] |= fl;
+}
+
+/* The shared-mode combination rule: an entry moves by the MEAN of the n
+ * contributions it received (this step's lanes, or the groups that changed it
+ * at a merge).  n == 1 is exact (so one lane reproduces the reference update);
+ * n > 1 divides in f64 and truncates toward zero — both correctly rounded
+ * IEEE operations, so host and gfx950 agree bit for bit. */
+static int64_t mean_delta(int64_t sum, int64_t n) {
+    if (n <= 1) return n == 1 ? sum : 0;
+    return (int64_t)trunc((double)sum / (double)n);
 }
 
 static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *rec) {
@@ -960,6 +975,7 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     /* ---- S-phase: TD update against the Q snapshot ---- */
     size_t nq = (size_t)b->P * b->S * A;
     memset(b->dq, 0, nq * 8);
+    memset(b->dc, 0, nq * 4);
     memset(b->df, 0, nq);
     for (uint32_t j = 0; j < nl; ++j) {
         lane_t *L = &b->lanes[lane0 + j];
@@ -1042,14 +1058,15 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     }
     if (b->priv) return;
     for (size_t k = 0; k < nq; ++k) {
-        b->q_g[k] = wrap_add(b->q_g[k], b->dq[k]);
+        b->q_g[k] = wrap_add(b->q_g[k], mean_delta(b->dq[k], b->dc[k]));
         b->f_g[k] |= b->df[k];
     }
 }
 
 static void run_launch(rlo_batch *b) {
     size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
-    memset(b->acc_q, 0, nq * 8); memset(b->acc_f, 0, nq); memset(b->acc_n, 0, nsa * 8);
+    memset(b->acc_q, 0, nq * 8); memset(b->acc_c, 0, nq * 8); memset(b->acc_f, 0, nq);
+    memset(b->acc_n, 0, nsa * 8);
     b->acc_t = 0;
     rlo_record *tmp = b->record ? (rlo_record *)malloc(sizeof(rlo_record) * b->G) : NULL;
     size_t rec0 = b->records.n;
@@ -1087,14 +1104,15 @@ static void run_launch(rlo_batch *b) {
             }
         }
         for (size_t i = 0; i < nq; ++i) {
-            b->acc_q[i] = wrap_add(b->acc_q[i], (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]));
+            const int64_t d = (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]);
+            if (d) { b->acc_q[i] = wrap_add(b->acc_q[i], d); b->acc_c[i] += 1; }
             b->acc_f[i] |= b->f_g[i];
         }
         for (size_t i = 0; i < nsa; ++i) b->acc_n[i] += (int64_t)b->n_g[i] - (int64_t)b->n_base[i];
         b->acc_t += (int64_t)(b->t_g - b->t_base);
     }
     for (size_t i = 0; i < nq; ++i) {
-        b->q_base[i] = wrap_add(b->q_base[i], b->acc_q[i]);
+        b->q_base[i] = wrap_add(b->q_base[i], mean_delta(b->acc_q[i], b->acc_c[i]));
         b->f_base[i] |= b->acc_f[i];
     }
     for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + b->acc_n[i]);

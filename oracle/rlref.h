@@ -22,7 +22,8 @@
  *      cpu_baseline.
  *   2. rlo_batch_*: the batched schedule the GPU implements (learner groups of
  *      G lanes, snapshot semantics per synchronous step, int64 fixed-point Q,
- *      merge every K steps).  G == 1 is the "private" mode: every lane is a
+ *      every entry moves by the MEAN of the deltas it received that step, and
+ *      every K steps the base moves by the mean of the groups' changes).  G == 1 is the "private" mode: every lane is a
  *      whole reference agent with its own f64 Q / UCB counters and no merging,
  *      so lane i reproduces (1) seeded with lane id i BIT-EXACTLY.  (Fixed
  *      point at G=1 only tracks (1) until a near-tie flips an argmax: f64

@@ -1,0 +1,377 @@
+// rl_device.h — gfx950 device building blocks of the tabular-RL hot path:
+// per-lane RNG stream, rand-0.8.5 distribution mappings, the shared ln(),
+// fixed-point Q, argmax/max and the four environments.
+//
+// Numerics contract (bit-exact with the CPU oracle and the reference's f64
+// arithmetic): no FP contraction, no fast-math; every expression keeps the
+// reference's evaluation order (citations inline).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_kparams.h"
+
+#pragma clang fp contract(off)
+
+namespace rlamd {
+
+constexpr double MIN_POSITIVE = 2.2250738585072014e-308;  // f64::MIN_POSITIVE
+
+// ------------------------------------------------------------------ RNG
+// Replaces rand::thread_rng() (entropy-seeded ChaCha12) at the reference's draw
+// sites with one xoshiro128** stream per lane, keyed (seed, global lane id).
+struct Rng {
+    uint32_t s0, s1, s2, s3;
+    __device__ __forceinline__ uint32_t next_u32() {
+        const uint32_t r = __builtin_rotateleft32(s1 * 5u, 7) * 9u;
+        const uint32_t t = s1 << 9;
+        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3;
+        s2 ^= t;
+        s3 = __builtin_rotateleft32(s3, 11);
+        return r;
+    }
+    // RngCore::next_u64 of a 32-bit block generator: low word first
+    __device__ __forceinline__ uint64_t next_u64() {
+        const uint64_t lo = next_u32();
+        const uint64_t hi = next_u32();
+        return lo | (hi << 32);
+    }
+};
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t &x) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint4 rng_seed(uint64_t seed, uint64_t lane) {
+    uint64_t x = seed + lane * 0x632BE59BD9B4E019ull;
+    const uint64_t a = splitmix64(x), b = splitmix64(x);
+    uint4 r = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    if ((r.x | r.y | r.z | r.w) == 0) r.x = 1;
+    return r;
+}
+
+// rand 0.8.5 UniformFloat<f64> for Uniform::from(0.0..1.0): ((u64>>12)|1.0) - 1.0
+__device__ __forceinline__ double uniform01(Rng &r) {
+    const uint64_t bits = (r.next_u64() >> 12) | 0x3FF0000000000000ull;
+    return __longlong_as_double((long long)bits) - 1.0;
+}
+// rand 0.8.5 UniformInt<usize>::sample for Uniform::from(0..A)
+// (uniform_epsilon_greed.rs:34,62): widening multiply, reject lo > zone.
+template <uint32_t A>
+__device__ __forceinline__ uint32_t uniform_action(Rng &r) {
+    constexpr uint64_t reject = (0ull - (uint64_t)A) % (uint64_t)A;  // (MAX - A + 1) % A
+    constexpr uint64_t zone = ~0ull - reject;
+    for (;;) {
+        const uint64_t v = r.next_u64();
+        const uint64_t lo = v * (uint64_t)A;
+        const uint64_t hi = __umul64hi(v, (uint64_t)A);
+        if (lo <= zone) return (uint32_t)hi;
+    }
+}
+// rand 0.8.5 UniformInt<u8>(1..11) with u32 large type (blackjack.rs:542,562)
+__device__ __forceinline__ uint32_t draw_card(Rng &r) {
+    constexpr uint32_t zone = 0xFFFFFFFFu - 6u;
+    for (;;) {
+        const uint64_t m = (uint64_t)r.next_u32() * 10u;
+        if ((uint32_t)m <= zone) return 1u + (uint32_t)(m >> 32);
+    }
+}
+
+// ------------------------------------------------------------------ ln()
+// fdlibm e_log.c operation sequence; the oracle (oracle/rlref.c rlo_log)
+// evaluates the identical sequence on the host, so UCB bonuses
+// (upper_confidence_bound.rs:36) agree bit for bit.
+__device__ inline double rl_log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                 Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01,
+                 Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+    uint64_t u = (uint64_t)__double_as_longlong(x);
+    int32_t hx = (int32_t)(u >> 32);
+    const uint32_t lx = (uint32_t)u;
+    int32_t k = 0;
+    if (hx < 0x00100000) {
+        if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -__builtin_inf();
+        if (hx < 0) return __builtin_nan("");
+        k -= 54;
+        x *= two54;
+        u = (uint64_t)__double_as_longlong(x);
+        hx = (int32_t)(u >> 32);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    int32_t i = (hx + 0x95f64) & 0x100000;
+    u = ((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (u & 0xffffffffull);
+    x = __longlong_as_double((long long)u);
+    k += (i >> 20);
+    const double f = x - 1.0;
+    double dk, R;
+    if ((0x000fffff & (2 + hx)) < 3) {
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    dk = (double)k;
+    const double z = s * s;
+    i = hx - 0x6147a;
+    const double w = z * z;
+    const int32_t j = 0x6b851 - hx;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    R = t2 + t1;
+    if (i > 0) {
+        const double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+// UCB value u_i = q_i + c * sqrt(ln(t) / (n_i + MIN_POSITIVE))
+// (upper_confidence_bound.rs:33-37,53-57); sqrt and / are correctly rounded.
+__device__ __forceinline__ double ucb_value(double q, double c, double lnt, double n) {
+    return q + c * __builtin_sqrt(lnt / (n + MIN_POSITIVE));
+}
+
+// ------------------------------------------------------------------ fixed-point Q
+__device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag) {
+    if (d != d) { flag |= QF_NAN; return 0; }
+    if (d == __builtin_inf()) { flag |= QF_PINF; return 0; }
+    if (d == -__builtin_inf()) { flag |= QF_NINF; return 0; }
+    const double x = d * 0x1p40;
+    if (x >= 0x1p62) return (int64_t)1 << 62;
+    if (x <= -0x1p62) return -((int64_t)1 << 62);
+    return (int64_t)__builtin_rint(x);
+}
+__device__ __forceinline__ double q_val(int64_t raw) { return (double)raw * 0x1p-40; }
+__device__ __forceinline__ double q_val(int64_t raw, uint32_t fl) {
+    if (fl) {
+        if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return __builtin_nan("");
+        return (fl & QF_PINF) ? __builtin_inf() : -__builtin_inf();
+    }
+    return (double)raw * 0x1p-40;
+}
+
+// ------------------------------------------------------------------ utils
+// argmax: first maximum, strict `>` (src/utils.rs:1-11)
+template <int A>
+__device__ __forceinline__ uint32_t argmax(const double (&v)[A]) {
+    double m = v[0];
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 1; i < A; ++i)
+        if (v[i] > m) { m = v[i]; r = (uint32_t)i; }
+    return r;
+}
+// max: src/utils.rs:13-21
+template <int A>
+__device__ __forceinline__ double vmax(const double (&v)[A]) {
+    double m = v[0];
+#pragma unroll
+    for (int i = 1; i < A; ++i)
+        if (v[i] > m) m = v[i];
+    return m;
+}
+// categorical_sample over a cumulative table: first i with cdf[i] > u, else 0
+// (src/utils.rs:33-43; the cdf is the reference's running sum, precomputed)
+__device__ __forceinline__ uint32_t cdf_search(const double *cdf, uint32_t n, double u) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    return lo < n ? lo : 0u;
+}
+
+// ------------------------------------------------------------------ environments
+// Lane env state: pos (dense obs), z (curr_step, or the Blackjack hand), ready.
+struct EnvTables {
+    const uint32_t *trans;
+    const double *cdf;
+    uint32_t n_start, max_steps;
+    double th1, th2, th3, trunc_reward;
+};
+
+template <int ENV> struct EnvDev;
+
+// FrozenLakeEnv (src/env/frozen_lake.rs).  trans[s*4+a]: 3 outcome bytes
+// (bits 0-5 next, bit 6 reward==1.0, bit 7 terminated) + bit 24 "slippery row".
+template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
+    static constexpr int A = 4;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
+        const double u = uniform01(r);                 // frozen_lake.rs:107-108
+        z = 0;
+        return cdf_search(t.cdf, t.n_start, u);
+    }
+    __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
+                                                const EnvTables &t, uint32_t &s2, double &rew,
+                                                bool &term) {
+        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :119-122
+        z += 1;
+        const uint32_t w = t.trans[pos * 4 + a];
+        const double u = uniform01(r);                 // :126, drawn even when not slippery
+        uint32_t i = 0;
+        if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
+        const uint32_t o = (w >> (8 * i)) & 0xffu;
+        s2 = o & 63u;
+        rew = (o & 64u) ? 1.0 : 0.0;
+        term = (o & 128u) != 0;
+        pos = s2;
+    }
+};
+
+// CliffWalkingEnv (src/env/cliff_walking.rs): deterministic, no RNG.
+// trans[s*4+a]: bits 0-5 next, bit 6 reward -100 (else -1), bit 7 terminated.
+template <> struct EnvDev<RL_ENV_CLIFF_WALKING> {
+    static constexpr int A = 4;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &, const EnvTables &) {
+        z = 0;
+        return 36u;                                    // cliff_walking.rs:71
+    }
+    __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
+                                                const EnvTables &t, uint32_t &s2, double &rew,
+                                                bool &term) {
+        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :81-84
+        z += 1;
+        const uint32_t w = t.trans[pos * 4 + a];
+        s2 = w & 63u;
+        rew = (w & 64u) ? -100.0 : -1.0;
+        term = (w & 128u) != 0;
+        pos = s2;
+    }
+};
+
+// TaxiEnv (src/env/taxi.rs): 500 states x 6 actions, deterministic table.
+// trans[s*6+a]: bits 0-8 next, bits 9-10 reward code {-1,-10,+20}, bit 11 terminated.
+template <> struct EnvDev<RL_ENV_TAXI> {
+    static constexpr int A = 6;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
+        const double u = uniform01(r);                 // taxi.rs:136-137
+        z = 0;
+        return cdf_search(t.cdf, t.n_start, u);
+    }
+    __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
+                                                const EnvTables &t, uint32_t &s2, double &rew,
+                                                bool &term) {
+        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :146-149
+        z += 1;
+        const uint32_t w = t.trans[pos * 6 + a];
+        s2 = w & 511u;
+        const uint32_t rc = (w >> 9) & 3u;
+        rew = rc == 0 ? -1.0 : (rc == 1 ? -10.0 : 20.0);
+        term = (w & (1u << 11)) != 0;
+        pos = s2;
+    }
+};
+
+// BlackJackEnv (src/env/blackjack.rs): infinite deck, cards 1..=10 uniform.
+// z packs the hand: bits 0-7 player sum, 8-15 dealer sum, 16-19 dealer[0],
+// bit 20 player_has_ace, bit 21 dealer_has_ace (aces from the first two cards
+// only, :54-55).  Dense obs = (p_score*27 + d_score)*2 + p_ace  (p <= 31, d <= 26).
+template <> struct EnvDev<RL_ENV_BLACKJACK> {
+    static constexpr int A = 2;
+    __device__ static __forceinline__ uint32_t score(uint32_t sum, uint32_t ace) {
+        return (ace && sum + 10u <= 21u) ? sum + 10u : sum;      // :58-74
+    }
+    __device__ static __forceinline__ uint32_t obs(uint32_t p, uint32_t d, uint32_t ace) {
+        return (p * 27u + d) * 2u + ace;
+    }
+    __device__ static __forceinline__ uint32_t deal(Rng &r) {    // initialize_hands :47-56
+        const uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
+        const uint32_t pa = (p0 == 1u || p1 == 1u), da = (d0 == 1u || d1 == 1u);
+        return (p0 + p1) | ((d0 + d1) << 8) | (d0 << 16) | (pa << 20) | (da << 21);
+    }
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &) {
+        z = deal(r);                                   // :105-116
+        const uint32_t pa = (z >> 20) & 1u;
+        return obs(score(z & 0xffu, pa), (z >> 16) & 0xfu, pa);
+    }
+    __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
+                                                const EnvTables &, uint32_t &s2, double &rew,
+                                                bool &term) {
+        uint32_t ps = z & 0xffu, ds = (z >> 8) & 0xffu;
+        const uint32_t d0 = (z >> 16) & 0xfu, pa = (z >> 20) & 1u, da = (z >> 21) & 1u;
+        if (a == 0) {                                  // hit :121-138
+            ps += draw_card(r);
+            const uint32_t p = score(ps, pa);
+            if (p > 21u) {
+                s2 = obs(p, score(ds, da), pa); rew = -1.0; term = true;
+            } else {
+                s2 = obs(p, d0, pa); rew = 0.0; term = false;
+            }
+        } else {                                       // stick :139-162
+            uint32_t d = score(ds, da);
+            while (d < 17u) {
+                ds += draw_card(r);
+                d = score(ds, da);
+            }
+            const uint32_t p = score(ps, pa);
+            s2 = obs(p, d, pa);
+            term = true;
+            rew = d > 21u ? 1.0 : (p > d ? 1.0 : (p < d ? -1.0 : 0.0));
+        }
+        z = ps | (ds << 8) | (z & 0xffff0000u);
+        pos = s2;
+    }
+};
+
+// ------------------------------------------------------------------ selection helpers
+// UniformEpsilonGreed::get_exploration_probs (uniform_epsilon_greed.rs:72-76)
+template <int A>
+__device__ __forceinline__ void eps_probs(double eps, const double (&q)[A], double (&p)[A]) {
+#pragma unroll
+    for (int i = 0; i < A; ++i) p[i] = eps / (double)A;
+    const uint32_t am = argmax<A>(q);
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+        if ((uint32_t)i == am) p[i] = 1.0 - eps;
+}
+// sarsa / qlearning / expected_sarsa (src/agent.rs:19-45)
+template <int A>
+__device__ __forceinline__ double future_q(int algo, const double (&q2)[A], uint32_t a2,
+                                           const double (&p)[A]) {
+    if (algo == RL_ALGO_SARSA) {
+        double v = q2[0];
+#pragma unroll
+        for (int i = 1; i < A; ++i)
+            if ((uint32_t)i == a2) v = q2[i];
+        return v;
+    }
+    if (algo == RL_ALGO_QLEARNING) return vmax<A>(q2);
+    double f = 0.0;
+#pragma unroll
+    for (int i = 0; i < A; ++i) f += p[i] * q2[i];
+    return f;
+}
+// decay_epsilon (uniform_epsilon_greed.rs:42-49) with the bins' closure
+__device__ __forceinline__ double decay_eps(const KParams &p, double eps) {
+    const double nw = p.decay_kind == RL_DECAY_MUL ? eps * p.eps_decay : eps - p.eps_decay;
+    return p.eps_final > nw ? eps : nw;
+}
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace rlamd

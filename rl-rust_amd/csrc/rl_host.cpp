@@ -1,0 +1,1015 @@
+// rl_host.cpp — host runtime behind include/rl.h: env table construction,
+// device memory layout, launch sequencing, the group merge, recording,
+// timing.  Everything compute-bearing runs in the gfx950 kernels; this file
+// only allocates, copies and launches.  There is no CPU fallback: without a
+// HIP device every compute entry point returns RL_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rl_kparams.h"
+
+using namespace rlamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPC(expr)                                                                                 \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(e_ == hipErrorOutOfMemory ? RL_E_OOM : RL_E_HIP,                           \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                        \
+    } while (0)
+
+// ------------------------------------------------------------------ env tables
+// The product's own construction of the reference envs (an independent
+// restatement from the oracle's and from tests/golden/make_tables.py).
+struct EnvHost {
+    int kind = 0;
+    uint32_t S = 0, A = 0, max_steps = 0;
+    std::vector<uint32_t> trans;  // packed, see rl_device.h EnvDev<>
+    std::vector<double> start;    // initial-state distribution
+    std::vector<double> cdf;      // running sum of `start` (categorical_sample, utils.rs:33-43)
+    double th1 = 0, th2 = 0, th3 = 0, trunc_reward = 0;
+};
+
+const char *const kFL4[] = {"SFFF", "FHFH", "FFFH", "HFFG"};                     // frozen_lake.rs:23
+const char *const kFL8[] = {"SFFFFFFF", "FFFFFFFF", "FFFHFFFF", "FFFFFHFF",       // frozen_lake.rs:25-28
+                            "FFFHFFFF", "FHHFFFHF", "FHFFHFHF", "FFFHFFFG"};
+const char *const kTaxiMap[] = {"+---------+", "|R: | : :G|", "| : | : : |", "| : : : : |",
+                                "| | : | : |", "|Y| : |B: |", "+---------+"};   // taxi.rs:22-30
+const int kTaxiLocs[4][2] = {{0, 0}, {0, 4}, {4, 0}, {4, 3}};                   // taxi.rs:31
+
+// utils::inc (src/utils.rs:53-76): 0 LEFT, 1 DOWN, 2 RIGHT, 3 UP, clamped
+void grid_move(int nrow, int ncol, int row, int col, int a, int &nr, int &nc) {
+    nr = row;
+    nc = col;
+    switch (a) {
+    case 0: nc = std::max(col - 1, 0); break;
+    case 1: nr = std::min(row + 1, nrow - 1); break;
+    case 2: nc = std::min(col + 1, ncol - 1); break;
+    case 3: nr = std::max(row - 1, 0); break;
+    default: break;
+    }
+}
+
+void finish_cdf(EnvHost &e) {
+    e.cdf.resize(e.start.size());
+    double b = 0.0;
+    for (size_t i = 0; i < e.start.size(); ++i) {
+        b += e.start[i];
+        e.cdf[i] = b;
+    }
+}
+
+int build_env(const rl_env_config &c, EnvHost &e) {
+    e = EnvHost();
+    e.kind = c.kind;
+    e.max_steps = c.max_steps;
+    if (c.kind == RL_ENV_FROZEN_LAKE) {
+        const char *const *map = c.map8x8 ? kFL8 : kFL4;
+        const int n = c.map8x8 ? 8 : 4;
+        e.S = n * n;
+        e.A = 4;
+        e.trans.assign(e.S * 4, 0);
+        int n_start = 0;
+        for (int i = 0; i < n * n; ++i) n_start += map[i / n][i % n] == 'S';
+        e.start.assign(e.S, 0.0);
+        for (int i = 0; i < n * n; ++i)
+            if (map[i / n][i % n] == 'S') e.start[i] = 1.0 / n_start;
+        auto outcome = [&](int row, int col, int a) -> uint32_t {
+            int nr, nc;
+            grid_move(n, n, row, col, a, nr, nc);
+            const char ch = map[nr][nc];
+            return (uint32_t)(nr * n + nc) | (ch == 'G' ? 64u : 0u) | ((ch == 'G' || ch == 'H') ? 128u : 0u);
+        };
+        for (int row = 0; row < n; ++row)
+            for (int col = 0; col < n; ++col)
+                for (int a = 0; a < 4; ++a) {
+                    const int s = row * n + col;
+                    const char ch = map[row][col];
+                    uint32_t w;
+                    if (ch == 'G' || ch == 'H') w = (uint32_t)s | 128u;              // (1.0, s, 0, true)
+                    else if (c.slippery)                                             // [(a-1)%4, a, (a+1)%4]
+                        w = outcome(row, col, (a + 3) & 3) | (outcome(row, col, a) << 8) |
+                            (outcome(row, col, (a + 1) & 3) << 16) | (1u << 24);
+                    else w = outcome(row, col, a);
+                    e.trans[s * 4 + a] = w;
+                }
+        const double third = 1.0 / 3.0;
+        e.th1 = 0.0 + third;
+        e.th2 = e.th1 + third;
+        e.th3 = e.th2 + third;
+        e.trunc_reward = 0.0;
+    } else if (c.kind == RL_ENV_CLIFF_WALKING) {
+        e.S = 48;
+        e.A = 4;
+        e.trans.assign(48 * 4, 0);
+        for (int row = 0; row < 4; ++row)
+            for (int col = 0; col < 12; ++col)
+                for (int a = 0; a < 4; ++a) {
+                    int nr, nc;
+                    grid_move(4, 12, row, col, a, nr, nc);
+                    const int ns = nr * 12 + nc;
+                    const bool cliff = ns >= 37 && ns <= 46, goal = ns == 47;  // cliff_walking.rs:9-11
+                    e.trans[(row * 12 + col) * 4 + a] =
+                        (uint32_t)ns | (cliff ? 64u : 0u) | ((cliff || goal) ? 128u : 0u);
+                }
+        e.start.assign(48, 0.0);
+        e.start[36] = 1.0;
+        e.trunc_reward = -100.0;
+    } else if (c.kind == RL_ENV_TAXI) {
+        e.S = 500;
+        e.A = 6;
+        e.trans.assign(500 * 6, 0);
+        e.start.assign(500, 0.0);
+        double total = 0.0;
+        auto enc = [](int r, int cc, int p, int d) { return ((r * 5 + cc) * 5 + p) * 4 + d; };
+        for (int r = 0; r < 5; ++r)
+            for (int cc = 0; cc < 5; ++cc)
+                for (int p = 0; p < 5; ++p)
+                    for (int d = 0; d < 4; ++d) {
+                        const int s = enc(r, cc, p, d);
+                        if (p < 4 && p != d) { e.start[s] += 1.0; total += 1.0; }
+                        for (int a = 0; a < 6; ++a) {
+                            int nr = r, nc = cc, np = p;
+                            uint32_t rcode = 0;  // -1
+                            bool term = false;
+                            if (a == 0) nr = std::min(r + 1, 4);
+                            else if (a == 1) nr = std::max(r - 1, 0);
+                            if (a == 2 && kTaxiMap[1 + r][2 * cc + 2] == ':') nc = std::min(cc + 1, 4);
+                            else if (a == 3 && kTaxiMap[1 + r][2 * cc] == ':') nc = std::max(cc - 1, 0);
+                            else if (a == 4) {
+                                if (p < 4 && r == kTaxiLocs[p][0] && cc == kTaxiLocs[p][1]) np = 4;
+                                else rcode = 1;  // -10
+                            } else if (a == 5) {
+                                if (r == kTaxiLocs[d][0] && cc == kTaxiLocs[d][1] && p == 4) {
+                                    np = d; term = true; rcode = 2;  // +20
+                                } else rcode = 1;
+                            }
+                            e.trans[s * 6 + a] = (uint32_t)enc(nr, nc, np, d) | (rcode << 9) | ((term ? 1u : 0u) << 11);
+                        }
+                    }
+        for (double &v : e.start) v /= total;   // taxi.rs:117-119
+        e.trunc_reward = 0.0;
+    } else if (c.kind == RL_ENV_BLACKJACK) {
+        e.S = 32 * 27 * 2;   // dense (p_score <= 31, d_score <= 26, p_ace)
+        e.A = 2;
+    } else {
+        return fail(RL_E_ARG, "unknown env kind");
+    }
+    if (!e.start.empty()) finish_cdf(e);
+    return RL_OK;
+}
+
+// value of a fixed-point Q entry (matches rlamd::q_val on the device)
+double q_value(int64_t raw, uint32_t fl) {
+    if (fl) {
+        if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return NAN;
+        return (fl & QF_PINF) ? INFINITY : -INFINITY;
+    }
+    return (double)raw * 0x1p-40;
+}
+int64_t q_fix(double d, uint32_t &flag) {
+    if (d != d) { flag |= QF_NAN; return 0; }
+    if (d == INFINITY) { flag |= QF_PINF; return 0; }
+    if (d == -INFINITY) { flag |= QF_NINF; return 0; }
+    const double x = d * 0x1p40;
+    if (x >= 0x1p62) return (int64_t)1 << 62;
+    if (x <= -0x1p62) return -((int64_t)1 << 62);
+    return (int64_t)std::rint(x);
+}
+
+template <class T>
+int dalloc(T **p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return RL_OK;
+    HIPC(hipMalloc((void **)p, n * sizeof(T)));
+    return RL_OK;
+}
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+// ====================================================================== handles
+struct rl_env {
+    rl_env_config cfg{};
+    EnvHost eh;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t L = 0;
+    uint4 *core = nullptr, *rng = nullptr;
+    uint32_t *trans = nullptr;
+    double *cdf = nullptr;
+    uint32_t *act_d = nullptr;
+    uint64_t *obs_d = nullptr;
+    double *rew_d = nullptr;
+    uint8_t *term_d = nullptr;
+    std::vector<uint8_t> ready;
+    KParams kp{};
+};
+
+struct rl_agent {
+    rl_agent_config cfg{};
+    EnvHost eh;
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    uint32_t S = 0, A = 0, P = 1, L = 0, G = 1, K = 1;
+    bool priv = false;
+    // lanes
+    uint4 *core = nullptr, *rng = nullptr, *aux = nullptr;
+    double *epi_reward = nullptr;
+    // shared
+    int64_t *q_base = nullptr;
+    uint32_t *qf_base = nullptr, *n_base = nullptr;
+    uint64_t *t_base = nullptr;
+    int64_t *delta_own = nullptr, *delta = nullptr;
+    uint64_t delta_words = 0;
+    // private
+    double *q_priv = nullptr;
+    uint32_t *n_priv = nullptr;
+    uint64_t *t_priv = nullptr;
+    // traces
+    double *trace = nullptr;
+    uint32_t *visited = nullptr;
+    uint32_t vis_words = 0;
+    // env tables
+    uint32_t *trans = nullptr;
+    double *cdf = nullptr;
+    // outputs
+    unsigned long long *stats_d = nullptr;
+    rl_step_record *rec_d = nullptr;
+    bool recording = false;
+    std::vector<rl_step_record> rec_h;
+    uint64_t launches = 0;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    KParams kp{};
+    train_launch_fn fn = nullptr;
+    dim3 grid, block;
+    size_t smem = 0;
+};
+
+namespace {
+
+int agent_select_kernel(rl_agent *a) {
+    a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->priv ? 1 : 0);
+    if (!a->fn) return fail(RL_E_ARG, "no kernel for this (env, agent, policy, selector)");
+    if (a->priv) {
+        a->block = dim3(256);
+        a->grid = dim3((a->L + 255) / 256);
+        a->smem = 0;
+        // tables only
+        const uint32_t SA = a->S * a->A;
+        size_t s = a->cfg.env.kind != RL_ENV_BLACKJACK ? ((SA * 4 + 15) & ~15u) : 0;
+        if (a->cfg.env.kind == RL_ENV_FROZEN_LAKE || a->cfg.env.kind == RL_ENV_TAXI)
+            s += (a->eh.cdf.size() * 8 + 15) & ~size_t(15);
+        a->smem = s;
+    } else {
+        const uint32_t g = std::min(a->G, a->L);
+        a->block = dim3(((g + 63) / 64) * 64);
+        a->grid = dim3((a->L + a->G - 1) / a->G);
+        a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
+                                    a->A, (uint32_t)a->eh.cdf.size());
+        if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
+    }
+    return RL_OK;
+}
+
+int agent_reset_policy(rl_agent *a) {
+    const size_t PSA = (size_t)a->P * a->S * a->A, SA = (size_t)a->S * a->A;
+    if (a->priv) {
+        launch_fill_f64(a->q_priv, PSA * a->L, a->cfg.q_default, a->stream);
+        HIPC(hipGetLastError());
+        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 4, a->stream));
+        if (a->t_priv) {
+            std::vector<uint64_t> ones(a->L, 1);
+            HIPC(hipMemcpyAsync(a->t_priv, ones.data(), a->L * 8, hipMemcpyHostToDevice, a->stream));
+            HIPC(hipStreamSynchronize(a->stream));
+        }
+    } else {
+        uint32_t fl = 0;
+        const int64_t d = q_fix(a->cfg.q_default, fl);
+        std::vector<int64_t> q(PSA, d);
+        std::vector<uint32_t> f(PSA, fl);
+        HIPC(hipMemcpyAsync(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipMemcpyAsync(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+    }
+    return RL_OK;
+}
+
+int agent_reset_selector(rl_agent *a) {
+    const size_t SA = (size_t)a->S * a->A;
+    if (a->priv) {
+        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 4, a->stream));
+        if (a->t_priv) {
+            std::vector<uint64_t> ones(a->L, 1);
+            HIPC(hipMemcpyAsync(a->t_priv, ones.data(), a->L * 8, hipMemcpyHostToDevice, a->stream));
+            HIPC(hipStreamSynchronize(a->stream));
+        }
+    } else {
+        HIPC(hipMemsetAsync(a->n_base, 0, SA * 4, a->stream));
+        const uint64_t one = 1;
+        HIPC(hipMemcpyAsync(a->t_base, &one, 8, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+    }
+    launch_arm_full(a->kp, -1, 0, 1, a->cfg.eps0, a->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+void agent_sync_params(rl_agent *a) {
+    KParams &p = a->kp;
+    p.lr = a->cfg.lr;
+    p.gamma = a->cfg.gamma;
+    p.gl = a->cfg.gamma * a->cfg.lambda;   // discount_factor * lambda_factor (elegibility_traces_agent.rs:94)
+    p.eps_decay = a->cfg.eps_decay;
+    p.eps_final = a->cfg.eps_final;
+    p.ucb_c = a->cfg.ucb_c;
+    p.decay_kind = a->cfg.decay_kind;
+    p.algo = a->cfg.algo;
+    p.delta = a->delta;
+}
+
+int launch_train_kernel(rl_agent *a) {
+    agent_sync_params(a);
+    if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (a->timing) {
+        HIPC(hipEventCreate(&e0));
+        HIPC(hipEventCreate(&e1));
+        HIPC(hipEventRecord(e0, a->stream));
+    }
+    {
+        const hipError_t le = a->fn(a->kp, a->grid, a->block, a->smem, a->stream);
+        if (le != hipSuccess)
+            return fail(RL_E_HIP, std::string("train kernel launch (smem ") + std::to_string(a->smem) +
+                                      " B, block " + std::to_string(a->block.x) + "): " + hipGetErrorString(le));
+    }
+    if (a->timing) {
+        HIPC(hipEventRecord(e1, a->stream));
+        a->events.emplace_back(e0, e1);
+    }
+    a->launches++;
+    if (a->recording) {
+        const size_t n = (size_t)a->K * a->L;
+        const size_t off = a->rec_h.size();
+        a->rec_h.resize(off + n);
+        HIPC(hipMemcpyAsync(a->rec_h.data() + off, a->rec_d, n * sizeof(rl_step_record),
+                            hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+    }
+    return RL_OK;
+}
+
+int launch_apply_kernel(rl_agent *a) {
+    if (a->priv) return RL_OK;
+    agent_sync_params(a);
+    const int spec = a->cfg.selector == RL_SEL_UCB && a->cfg.algo == RL_ALGO_EXPECTED_SARSA;
+    launch_apply(a->kp, spec, a->stream);
+    HIPC(hipGetLastError());
+    return RL_OK;
+}
+
+int run_until_done(rl_agent *a, rl_stats *out) {
+    // stats slot 5 counts lanes that are DONE at the end of a launch
+    for (;;) {
+        HIPC(hipMemsetAsync(&a->stats_d[5], 0, 8, a->stream));
+        int rc = launch_train_kernel(a);
+        if (rc) return rc;
+        rc = launch_apply_kernel(a);
+        if (rc) return rc;
+        unsigned long long done = 0;
+        HIPC(hipMemcpyAsync(&done, &a->stats_d[5], 8, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+        if (const char *dump = getenv("RLAMD_DEBUG_LANES")) {   // diagnostics: raw lane records per launch
+            std::vector<uint4> c(a->L);
+            HIPC(hipMemcpy(c.data(), a->core, a->L * 16, hipMemcpyDeviceToHost));
+            if (FILE *f = fopen(dump, "ab")) { fwrite(c.data(), 16, a->L, f); fclose(f); }
+        }
+        if (done >= a->L) break;
+    }
+    if (out) return rl_agent_stats(a, out);
+    return RL_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char *rl_last_error(void) { return g_err.c_str(); }
+int rl_abi_version(void) { return RL_ABI_VERSION; }
+int rl_device_count(int *count) {
+    HIPC(hipGetDeviceCount(count));
+    return RL_OK;
+}
+
+uint64_t rl_blackjack_obs_id(uint32_t p, uint32_t d, uint32_t ace) {
+    // fxhash 0.2.1: FxHasher64::write_u8 per field of #[derive(Hash)]
+    const uint64_t K = 0x517cc1b727220a95ull;
+    uint64_t h = 0;
+    const uint64_t w[3] = {p & 0xffu, d & 0xffu, ace ? 1u : 0u};
+    for (uint64_t x : w) h = (((h << 5) | (h >> 59)) ^ x) * K;
+    return h;
+}
+uint64_t rl_obs_to_reference(int32_t env_kind, uint32_t s) {
+    if (env_kind == RL_ENV_BLACKJACK) return rl_blackjack_obs_id(s / 54u, (s >> 1) % 27u, s & 1u);
+    return s;
+}
+
+int rl_env_dims(const rl_env_config *cfg, uint32_t *S, uint32_t *A) {
+    if (!cfg || !S || !A) return fail(RL_E_ARG, "null argument");
+    EnvHost e;
+    int rc = build_env(*cfg, e);
+    if (rc) return rc;
+    *S = e.S;
+    *A = e.A;
+    return RL_OK;
+}
+
+int rl_env_table(const rl_env_config *cfg, double *prob, uint32_t *next, double *reward, uint8_t *term,
+                 double *start) {
+    if (!cfg) return fail(RL_E_ARG, "null config");
+    EnvHost e;
+    int rc = build_env(*cfg, e);
+    if (rc) return rc;
+    if (e.kind == RL_ENV_BLACKJACK) return fail(RL_E_ARG, "Blackjack has no transition table");
+    for (uint32_t s = 0; s < e.S; ++s)
+        for (uint32_t a = 0; a < e.A; ++a) {
+            const uint32_t w = e.trans[s * e.A + a];
+            const size_t k = ((size_t)s * e.A + a) * 3;
+            double pr[3] = {1.0, 0.0, 0.0};
+            uint32_t nx[3] = {0, 0, 0};
+            double rw[3] = {0.0, 0.0, 0.0};
+            uint8_t tm[3] = {0, 0, 0};
+            if (e.kind == RL_ENV_FROZEN_LAKE) {
+                const int n = (w >> 24) & 1 ? 3 : 1;
+                for (int i = 0; i < n; ++i) {
+                    const uint32_t o = (w >> (8 * i)) & 0xffu;
+                    pr[i] = n == 3 ? 1.0 / 3.0 : 1.0;
+                    nx[i] = o & 63u;
+                    rw[i] = (o & 64u) ? 1.0 : 0.0;
+                    tm[i] = (o & 128u) ? 1 : 0;
+                }
+            } else if (e.kind == RL_ENV_CLIFF_WALKING) {
+                nx[0] = w & 63u;
+                rw[0] = (w & 64u) ? -100.0 : -1.0;
+                tm[0] = (w & 128u) ? 1 : 0;
+            } else {
+                nx[0] = w & 511u;
+                const uint32_t rc2 = (w >> 9) & 3u;
+                rw[0] = rc2 == 0 ? -1.0 : (rc2 == 1 ? -10.0 : 20.0);
+                tm[0] = (w >> 11) & 1u;
+            }
+            for (int i = 0; i < 3; ++i) {
+                if (prob) prob[k + i] = pr[i];
+                if (next) next[k + i] = nx[i];
+                if (reward) reward[k + i] = rw[i];
+                if (term) term[k + i] = tm[i];
+            }
+        }
+    if (start) std::memcpy(start, e.start.data(), e.S * sizeof(double));
+    return RL_OK;
+}
+
+// ---------------------------------------------------------------- Env
+int rl_env_create(const rl_env_config *cfg, uint32_t n, uint64_t seed, uint64_t lane_offset, int32_t device,
+                  rl_env **out) {
+    if (!cfg || !out || n == 0) return fail(RL_E_ARG, "bad argument");
+    *out = nullptr;
+    rl_env *e = new rl_env();
+    e->cfg = *cfg;
+    int rc = build_env(*cfg, e->eh);
+    if (rc) { delete e; return rc; }
+    e->device = device;
+    e->L = n;
+    auto bad = [&](int code) { rl_env_destroy(e); return code; };
+    if (hipSetDevice(device) != hipSuccess) return bad(fail(RL_E_HIP, "hipSetDevice failed (no GPU?)"));
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+        return bad(fail(RL_E_HIP, "hipStreamCreate failed"));
+    if ((rc = dalloc(&e->core, n)) || (rc = dalloc(&e->rng, n)) || (rc = dalloc(&e->act_d, n)) ||
+        (rc = dalloc(&e->obs_d, n)) || (rc = dalloc(&e->rew_d, n)) || (rc = dalloc(&e->term_d, n)) ||
+        (rc = dalloc(&e->trans, e->eh.trans.size())) || (rc = dalloc(&e->cdf, e->eh.cdf.size())))
+        return bad(rc);
+    if (!e->eh.trans.empty() &&
+        hipMemcpy(e->trans, e->eh.trans.data(), e->eh.trans.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bad(fail(RL_E_HIP, "table upload"));
+    if (!e->eh.cdf.empty() &&
+        hipMemcpy(e->cdf, e->eh.cdf.data(), e->eh.cdf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return bad(fail(RL_E_HIP, "table upload"));
+    KParams &p = e->kp;
+    p.L = n; p.S = e->eh.S; p.A = e->eh.A; p.P = 1;
+    p.core = e->core; p.rng = e->rng;
+    p.trans = e->trans; p.start_cdf = e->cdf; p.n_start = (uint32_t)e->eh.cdf.size();
+    p.max_steps = e->eh.max_steps; p.th1 = e->eh.th1; p.th2 = e->eh.th2; p.th3 = e->eh.th3;
+    p.trunc_reward = e->eh.trunc_reward;
+    // lane init needs aux/epi_reward: use scratch
+    uint4 *aux = nullptr;
+    double *er = nullptr;
+    if ((rc = dalloc(&aux, n)) || (rc = dalloc(&er, n))) return bad(rc);
+    p.aux = aux; p.epi_reward = er;
+    launch_lane_init(cfg->kind, p, seed, lane_offset, 0.0, e->stream);
+    hipError_t he = hipStreamSynchronize(e->stream);
+    dfree(aux);
+    dfree(er);
+    p.aux = nullptr; p.epi_reward = nullptr;
+    if (he != hipSuccess) return bad(fail(RL_E_HIP, hipGetErrorString(he)));
+    e->ready.assign(n, 0);
+    *out = e;
+    return RL_OK;
+}
+
+void rl_env_destroy(rl_env *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    dfree(e->core); dfree(e->rng); dfree(e->act_d); dfree(e->obs_d); dfree(e->rew_d); dfree(e->term_d);
+    dfree(e->trans); dfree(e->cdf);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int rl_env_reset(rl_env *e, uint64_t *obs) {
+    if (!e || !obs) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(e->device));
+    launch_env_reset(e->cfg.kind, e->kp, e->stream, e->obs_d);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < e->L; ++i) obs[i] = rl_obs_to_reference(e->cfg.kind, (uint32_t)obs[i]);
+    std::fill(e->ready.begin(), e->ready.end(), 1);
+    return RL_OK;
+}
+
+int rl_env_step(rl_env *e, const uint32_t *act, uint64_t *obs, double *rew, uint8_t *term) {
+    if (!e || !act || !obs || !rew || !term) return fail(RL_E_ARG, "null argument");
+    for (uint32_t i = 0; i < e->L; ++i) {
+        if (!e->ready[i]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(i));
+        if (act[i] >= e->eh.A) return fail(RL_E_ARG, "action out of range");
+    }
+    HIPC(hipSetDevice(e->device));
+    HIPC(hipMemcpyAsync(e->act_d, act, e->L * 4, hipMemcpyHostToDevice, e->stream));
+    launch_env_step(e->cfg.kind, e->kp, e->stream, e->act_d, e->obs_d, e->rew_d, e->term_d, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipMemcpyAsync(rew, e->rew_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipMemcpyAsync(term, e->term_d, e->L, hipMemcpyDeviceToHost, e->stream));
+    HIPC(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < e->L; ++i) {
+        obs[i] = rl_obs_to_reference(e->cfg.kind, (uint32_t)obs[i]);
+        if (term[i]) e->ready[i] = 0;
+    }
+    return RL_OK;
+}
+
+// ---------------------------------------------------------------- Agent
+int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
+    if (!cfg || !out) return fail(RL_E_ARG, "null argument");
+    *out = nullptr;
+    const rl_agent_config &c = *cfg;
+    if (c.n_lanes == 0 || c.group_size == 0 || c.group_size > 1024 || c.sync_every == 0)
+        return fail(RL_E_ARG, "need n_lanes >= 1, 1 <= group_size <= 1024, sync_every >= 1");
+    if (c.agent < 0 || c.agent > 1 || c.policy < 0 || c.policy > 1 || c.selector < 0 || c.selector > 1 ||
+        c.algo < 0 || c.algo > 2 || c.decay_kind < 0 || c.decay_kind > 1)
+        return fail(RL_E_ARG, "enum out of range");
+    rl_agent *a = new rl_agent();
+    a->cfg = c;
+    int rc = build_env(c.env, a->eh);
+    if (rc) { delete a; return rc; }
+    auto bad = [&](int code) { rl_agent_destroy(a); return code; };
+    a->device = c.device;
+    a->S = a->eh.S; a->A = a->eh.A; a->P = c.policy == RL_POLICY_DOUBLE ? 2 : 1;
+    a->L = c.n_lanes; a->G = c.group_size; a->K = c.sync_every;
+    a->priv = a->G == 1;
+    if (hipSetDevice(c.device) != hipSuccess) return bad(fail(RL_E_HIP, "hipSetDevice failed (no GPU?)"));
+    if (hipStreamCreateWithFlags(&a->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return bad(fail(RL_E_HIP, "hipStreamCreate failed"));
+    a->stream = a->own_stream;
+    const size_t L = a->L, SA = (size_t)a->S * a->A, PSA = a->P * SA;
+    if ((rc = dalloc(&a->core, L)) || (rc = dalloc(&a->rng, L)) || (rc = dalloc(&a->aux, L)) ||
+        (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, 8)) ||
+        (rc = dalloc(&a->trans, a->eh.trans.size())) || (rc = dalloc(&a->cdf, a->eh.cdf.size())))
+        return bad(rc);
+    if (a->priv) {
+        if ((rc = dalloc(&a->q_priv, PSA * L))) return bad(rc);
+        // UCB counters are allocated even for eps-greedy: set_action_selector may switch
+        if ((rc = dalloc(&a->n_priv, SA * L)) || (rc = dalloc(&a->t_priv, L))) return bad(rc);
+    } else {
+        a->delta_words = 2 * PSA + SA + 1 + 3 * PSA;
+        if ((rc = dalloc(&a->q_base, PSA)) || (rc = dalloc(&a->qf_base, PSA)) || (rc = dalloc(&a->n_base, SA)) ||
+            (rc = dalloc(&a->t_base, 1)) || (rc = dalloc(&a->delta_own, a->delta_words)))
+            return bad(rc);
+        a->delta = a->delta_own;
+        if (hipMemset(a->delta, 0, a->delta_words * 8) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+    }
+    if (c.agent == RL_AGENT_TRACES) {
+        a->vis_words = (a->S + 31) / 32;
+        if ((rc = dalloc(&a->trace, SA * L)) || (rc = dalloc(&a->visited, (size_t)a->vis_words * L))) return bad(rc);
+        if (hipMemset(a->trace, 0, SA * L * 8) != hipSuccess || hipMemset(a->visited, 0, (size_t)a->vis_words * L * 4) != hipSuccess)
+            return bad(fail(RL_E_HIP, "memset"));
+    }
+    if (!a->eh.trans.empty() &&
+        hipMemcpy(a->trans, a->eh.trans.data(), a->eh.trans.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bad(fail(RL_E_HIP, "table upload"));
+    if (!a->eh.cdf.empty() &&
+        hipMemcpy(a->cdf, a->eh.cdf.data(), a->eh.cdf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return bad(fail(RL_E_HIP, "table upload"));
+    if (hipMemset(a->stats_d, 0, 64) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+
+    KParams &p = a->kp;
+    p.L = a->L; p.G = a->G; p.K = a->K; p.S = a->S; p.A = a->A; p.P = a->P;
+    p.core = a->core; p.rng = a->rng; p.aux = a->aux; p.epi_reward = a->epi_reward;
+    p.q_base = a->q_base; p.qf_base = a->qf_base; p.n_base = a->n_base; p.t_base = a->t_base;
+    p.delta = a->delta;
+    p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
+    p.trace = a->trace; p.visited = a->visited; p.vis_words = a->vis_words;
+    p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
+    p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
+    p.trunc_reward = a->eh.trunc_reward;
+    p.target_episodes = 0; p.eval_at = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;
+    p.stats = a->stats_d;
+    p.rec = nullptr;
+    agent_sync_params(a);
+    if ((rc = agent_select_kernel(a))) return bad(rc);
+    launch_lane_init(c.env.kind, p, c.seed, c.lane_offset, c.eps0, a->stream);
+    if (hipGetLastError() != hipSuccess) return bad(fail(RL_E_HIP, "lane init launch"));
+    if ((rc = agent_reset_policy(a))) return bad(rc);
+    if ((rc = agent_reset_selector(a))) return bad(rc);
+    *out = a;
+    return RL_OK;
+}
+
+void rl_agent_destroy(rl_agent *a) {
+    if (!a) return;
+    (void)hipSetDevice(a->device);
+    if (a->own_stream) (void)hipStreamSynchronize(a->own_stream);
+    for (auto &ev : a->events) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+    dfree(a->core); dfree(a->rng); dfree(a->aux); dfree(a->epi_reward);
+    dfree(a->q_base); dfree(a->qf_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own);
+    dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
+    dfree(a->trace); dfree(a->visited); dfree(a->trans); dfree(a->cdf);
+    dfree(a->stats_d); dfree(a->rec_d);
+    if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
+    delete a;
+}
+
+int rl_agent_set_future_q_value_func(rl_agent *a, int32_t algo) {
+    if (!a || algo < 0 || algo > 2) return fail(RL_E_ARG, "bad algo");
+    a->cfg.algo = algo;
+    agent_sync_params(a);
+    return RL_OK;
+}
+
+int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double eps_decay, double eps_final,
+                                 int32_t decay_kind, double ucb_c) {
+    if (!a || sel < 0 || sel > 1 || decay_kind < 0 || decay_kind > 1) return fail(RL_E_ARG, "bad selector");
+    HIPC(hipSetDevice(a->device));
+    a->cfg.selector = sel;
+    a->cfg.eps0 = eps0; a->cfg.eps_decay = eps_decay; a->cfg.eps_final = eps_final;
+    a->cfg.decay_kind = decay_kind; a->cfg.ucb_c = ucb_c;
+    agent_sync_params(a);
+    int rc = agent_select_kernel(a);
+    if (rc) return rc;
+    return agent_reset_selector(a);
+}
+
+int rl_agent_reset(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    int rc = agent_reset_policy(a);
+    if (rc) return rc;
+    return agent_reset_selector(a);
+}
+
+int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    if (a->trace) {
+        HIPC(hipMemsetAsync(a->trace, 0, (size_t)a->S * a->A * a->L * 8, a->stream));
+        HIPC(hipMemsetAsync(a->visited, 0, (size_t)a->vis_words * a->L * 4, a->stream));
+    }
+    launch_arm_full(a->kp, n_episodes ? RL_MODE_TRAIN : RL_MODE_DONE, 0, 0, 0.0, a->stream);
+    HIPC(hipGetLastError());
+    if (n_episodes == 0) {
+        HIPC(hipStreamSynchronize(a->stream));
+        return out ? rl_agent_stats(a, out) : RL_OK;
+    }
+    a->kp.target_episodes = n_episodes;
+    a->kp.eval_at = eval_at;
+    a->kp.eval_only = 0;
+    int rc = run_until_done(a, out);
+    a->kp.target_episodes = 0;
+    a->kp.eval_at = 0;
+    return rc;
+}
+
+int rl_agent_evaluate(rl_agent *a, uint64_t n_episodes, rl_stats *out) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    if (n_episodes == 0) return out ? rl_agent_stats(a, out) : RL_OK;
+    if (n_episodes > 0xffffffffull) return fail(RL_E_ARG, "too many evaluation episodes");
+    launch_arm_full(a->kp, RL_MODE_EVAL, (uint32_t)n_episodes, 0, 0.0, a->stream);
+    HIPC(hipGetLastError());
+    a->kp.target_episodes = 0;
+    a->kp.eval_at = 0;
+    a->kp.eval_only = 1;
+    int rc = run_until_done(a, out);
+    a->kp.eval_only = 0;
+    if (rc) return rc;
+    // back to training mode (lanes start a new episode on the next call)
+    launch_arm_full(a->kp, RL_MODE_TRAIN, 0, 0, 0.0, a->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_run(rl_agent *a, uint32_t n) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    for (uint32_t i = 0; i < n; ++i) {
+        int rc = launch_train_kernel(a);
+        if (rc) return rc;
+        rc = launch_apply_kernel(a);
+        if (rc) return rc;
+    }
+    return RL_OK;
+}
+
+int rl_agent_synchronize(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_stats(rl_agent *a, rl_stats *out) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    unsigned long long s[8];
+    HIPC(hipMemcpyAsync(s, a->stats_d, 64, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    out->train_steps = s[0];
+    out->eval_steps = s[1];
+    out->train_episodes = s[2];
+    out->eval_episodes = s[3];
+    out->reward_sum_q16 = (int64_t)s[4];
+    out->done_lanes = s[5];
+    out->launches = a->launches;
+    out->reserved = 0;
+    return RL_OK;
+}
+
+int rl_agent_dims(rl_agent *a, uint32_t *S, uint32_t *A, uint32_t *P) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (S) *S = a->S;
+    if (A) *A = a->A;
+    if (P) *P = a->P;
+    return RL_OK;
+}
+
+int rl_agent_lane_state(rl_agent *a, uint32_t *core, uint32_t *aux, size_t n) {
+    if (!a || n < a->L) return fail(RL_E_ARG, "bad argument");
+    HIPC(hipSetDevice(a->device));
+    if (core) HIPC(hipMemcpyAsync(core, a->core, a->L * 16, hipMemcpyDeviceToHost, a->stream));
+    if (aux) HIPC(hipMemcpyAsync(aux, a->aux, a->L * 16, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    if (a->priv) {
+        if (n < PSA * a->L) return fail(RL_E_ARG, "output too small: need n_lanes*P*S*A");
+        std::vector<double> tmp(PSA * a->L);
+        HIPC(hipMemcpyAsync(tmp.data(), a->q_priv, tmp.size() * 8, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+        for (size_t e = 0; e < PSA; ++e)
+            for (size_t l = 0; l < a->L; ++l) out[l * PSA + e] = tmp[e * a->L + l];
+        return RL_OK;
+    }
+    if (n < PSA) return fail(RL_E_ARG, "output too small: need P*S*A");
+    std::vector<int64_t> q(PSA);
+    std::vector<uint32_t> f(PSA);
+    HIPC(hipMemcpyAsync(q.data(), a->q_base, PSA * 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipMemcpyAsync(f.data(), a->qf_base, PSA * 4, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (size_t i = 0; i < PSA; ++i) out[i] = q_value(q[i], f[i]);
+    return RL_OK;
+}
+
+int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
+    if (!a || !in) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    if (a->priv) {
+        if (n < PSA * a->L) return fail(RL_E_ARG, "input too small");
+        std::vector<double> tmp(PSA * a->L);
+        for (size_t e = 0; e < PSA; ++e)
+            for (size_t l = 0; l < a->L; ++l) tmp[e * a->L + l] = in[l * PSA + e];
+        HIPC(hipMemcpy(a->q_priv, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice));
+        return RL_OK;
+    }
+    if (n < PSA) return fail(RL_E_ARG, "input too small");
+    std::vector<int64_t> q(PSA);
+    std::vector<uint32_t> f(PSA, 0);
+    for (size_t i = 0; i < PSA; ++i) q[i] = q_fix(in[i], f[i]);
+    HIPC(hipMemcpy(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice));
+    return RL_OK;
+}
+
+int rl_agent_get_q_raw(rl_agent *a, int64_t *out, size_t n) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    if (a->priv) return fail(RL_E_STATE, "private mode (group_size 1) keeps f64 Q");
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    if (n < PSA) return fail(RL_E_ARG, "output too small");
+    HIPC(hipSetDevice(a->device));
+    HIPC(hipMemcpyAsync(out, a->q_base, PSA * 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_get_ucb(rl_agent *a, uint32_t *counts, size_t nc, uint64_t *t, size_t nt) {
+    if (!a || !counts || !t) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    const size_t SA = (size_t)a->S * a->A;
+    if (a->priv) {
+        if (nc < SA * a->L || nt < a->L) return fail(RL_E_ARG, "output too small");
+        std::vector<uint32_t> tmp(SA * a->L);
+        HIPC(hipMemcpyAsync(tmp.data(), a->n_priv, tmp.size() * 4, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipMemcpyAsync(t, a->t_priv, a->L * 8, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+        for (size_t e = 0; e < SA; ++e)
+            for (size_t l = 0; l < a->L; ++l) counts[l * SA + e] = tmp[e * a->L + l];
+        return RL_OK;
+    }
+    if (nc < SA || nt < 1) return fail(RL_E_ARG, "output too small");
+    HIPC(hipMemcpyAsync(counts, a->n_base, SA * 4, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipMemcpyAsync(t, a->t_base, 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n) {
+    if (!a || !out || n < a->L) return fail(RL_E_ARG, "bad argument");
+    HIPC(hipSetDevice(a->device));
+    std::vector<uint4> x(a->L);
+    HIPC(hipMemcpyAsync(x.data(), a->aux, a->L * 16, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (size_t i = 0; i < a->L; ++i) {
+        const uint64_t b = ((uint64_t)x[i].y << 32) | x[i].x;
+        std::memcpy(&out[i], &b, 8);
+    }
+    return RL_OK;
+}
+
+int rl_agent_set_recording(rl_agent *a, int32_t enable) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    if (enable && !a->rec_d) {
+        int rc = dalloc(&a->rec_d, (size_t)a->K * a->L);
+        if (rc) return rc;
+    }
+    a->recording = enable != 0;
+    return RL_OK;
+}
+
+int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64_t *n_total) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (n_total) *n_total = a->rec_h.size();
+    if (out) {
+        const size_t n = std::min<size_t>(cap, a->rec_h.size());
+        std::memcpy(out, a->rec_h.data(), n * sizeof(rl_step_record));
+        a->rec_h.clear();
+    }
+    return RL_OK;
+}
+
+int rl_agent_delta_words(rl_agent *a, uint64_t *n) {
+    if (!a || !n) return fail(RL_E_ARG, "null argument");
+    *n = a->delta_words;
+    return RL_OK;
+}
+
+int rl_agent_set_delta_buffer(rl_agent *a, void *ptr, uint64_t n_words) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (a->priv) return fail(RL_E_STATE, "private mode has no merge");
+    if (ptr == nullptr) { a->delta = a->delta_own; agent_sync_params(a); return RL_OK; }
+    if (n_words < a->delta_words) return fail(RL_E_ARG, "delta buffer too small");
+    a->delta = (int64_t *)ptr;
+    agent_sync_params(a);
+    return RL_OK;
+}
+
+int rl_agent_launch_train(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    return launch_train_kernel(a);
+}
+
+int rl_agent_launch_apply(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    return launch_apply_kernel(a);
+}
+
+int rl_agent_set_stream(rl_agent *a, void *stream) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    a->stream = stream ? (hipStream_t)stream : a->own_stream;
+    return RL_OK;
+}
+
+int rl_agent_set_timing(rl_agent *a, int32_t enable) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    a->timing = enable != 0;
+    return RL_OK;
+}
+
+int rl_agent_get_timing(rl_agent *a, double *total_ms, uint64_t *n) {
+    if (!a || !total_ms || !n) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    HIPC(hipStreamSynchronize(a->stream));
+    double tot = 0.0;
+    for (auto &ev : a->events) {
+        float ms = 0.f;
+        HIPC(hipEventElapsedTime(&ms, ev.first, ev.second));
+        tot += ms;
+        (void)hipEventDestroy(ev.first);
+        (void)hipEventDestroy(ev.second);
+    }
+    *n = a->events.size();
+    *total_ms = tot;
+    a->events.clear();
+    return RL_OK;
+}
+
+// ---------------------------------------------------------------- KAT probes
+int rl_kat_log(int32_t device, const double *x, double *out, uint32_t n) {
+    if (!x || !out) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(device));
+    double *dx = nullptr, *dy = nullptr;
+    HIPC(hipMalloc(&dx, n * 8ull));
+    HIPC(hipMalloc(&dy, n * 8ull));
+    HIPC(hipMemcpy(dx, x, n * 8ull, hipMemcpyHostToDevice));
+    launch_kat_log(dx, dy, n, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpy(out, dy, n * 8ull, hipMemcpyDeviceToHost));
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    return RL_OK;
+}
+
+int rl_kat_rng(int32_t device, uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out) {
+    if (!out) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(device));
+    uint32_t *d = nullptr;
+    HIPC(hipMalloc(&d, n * 4ull));
+    launch_kat_rng(seed, lane, n, d, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpy(out, d, n * 4ull, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return RL_OK;
+}
+
+int rl_kat_ucb(int32_t device, const double *q, const double *nc, const uint64_t *t, double c, double *out,
+               uint32_t n) {
+    if (!q || !nc || !t || !out) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(device));
+    double *dq = nullptr, *dn = nullptr, *dy = nullptr;
+    uint64_t *dt = nullptr;
+    HIPC(hipMalloc(&dq, n * 8ull));
+    HIPC(hipMalloc(&dn, n * 8ull));
+    HIPC(hipMalloc(&dy, n * 8ull));
+    HIPC(hipMalloc(&dt, n * 8ull));
+    HIPC(hipMemcpy(dq, q, n * 8ull, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(dn, nc, n * 8ull, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(dt, t, n * 8ull, hipMemcpyHostToDevice));
+    launch_kat_ucb(dq, dn, dt, c, dy, n, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpy(out, dy, n * 8ull, hipMemcpyDeviceToHost));
+    (void)hipFree(dq); (void)hipFree(dn); (void)hipFree(dy); (void)hipFree(dt);
+    return RL_OK;
+}
+
+}  // extern "C"

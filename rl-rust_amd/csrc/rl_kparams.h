@@ -1,0 +1,88 @@
+// rl_kparams.h — kernel parameter block and lane-record packing shared by the
+// host runtime (rl_host.cpp) and the gfx950 kernels (rl_train_*.hip).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#include "rl.h"
+
+namespace rlamd {
+
+// Q fixed point for the shared (group_size > 1) mode: value = raw * 2^-QFRAC.
+constexpr int QFRAC = 40;
+// sticky non-finite flags of a fixed-point Q entry (IEEE sum algebra, order free)
+constexpr uint32_t QF_NAN = 1u, QF_PINF = 2u, QF_NINF = 4u;
+
+// lane core record (uint4, SoA over lanes):
+//   x = s (dense state), y = flags word below, z = env word (curr_step | blackjack hand),
+//   w = training episodes finished in the current train() call
+constexpr uint32_t LF_ACT_MASK = 0xffu;
+constexpr uint32_t LF_NEED_RESET = 1u << 8;
+constexpr uint32_t LF_READY = 1u << 9;
+constexpr uint32_t LF_DFLAG = 1u << 10;   // DoubleTabularPolicy::policy_flag (starts true)
+constexpr int LF_MODE_SHIFT = 12;         // rl_lane_mode, 2 bits
+// lane aux record (uint4): x,y = epsilon (f64 bits), z = eval episodes left, w = episode length
+
+struct KParams {
+    uint32_t L, G, K, S, A, P;
+    // lanes
+    uint4 *core;
+    uint4 *rng;
+    uint4 *aux;
+    double *epi_reward;
+    // shared mode
+    int64_t *q_base;       // [P][S][A]
+    uint32_t *qf_base;     // [P][S][A]
+    uint32_t *n_base;      // [S][A]
+    uint64_t *t_base;      // [1]
+    int64_t *delta;        // [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
+    // private mode (SoA [entry][lane])
+    double *q_priv;
+    uint32_t *n_priv;
+    uint64_t *t_priv;      // [L]
+    // eligibility traces (SoA [entry][lane])
+    double *trace;
+    uint32_t *visited;     // [words][L]
+    uint32_t vis_words;
+    // env tables
+    const uint32_t *trans; // [S][A] packed
+    const double *start_cdf;
+    uint32_t n_start;
+    uint32_t max_steps;
+    double th1, th2, th3;  // slippery FrozenLake cumulative sums
+    double trunc_reward;
+    // hyper-parameters
+    double lr, gamma, gl, eps_decay, eps_final, ucb_c;
+    int32_t decay_kind, algo;
+    // train()/evaluate() control
+    uint64_t target_episodes, eval_at;
+    uint32_t eval_episodes;
+    int32_t eval_only;
+    // outputs
+    unsigned long long *stats; // rl_stats as u64[8]
+    rl_step_record *rec;       // [K][L] or null
+};
+
+// one entry per (env, agent, policy, selector, private) kernel instantiation
+typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, size_t smem,
+                                      hipStream_t stream);
+
+train_launch_fn lookup_train(int env, int agent, int policy, int sel, int priv);
+size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
+
+// env-only kernels (batched Env trait) and KAT probes
+void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs);
+void launch_env_step(int env, const KParams &p, hipStream_t s, const uint32_t *act, uint64_t *obs,
+                     double *rew, uint8_t *term, unsigned int *not_ready);
+void launch_lane_init(int env, const KParams &p, uint64_t seed, uint64_t lane_offset, double eps0,
+                      hipStream_t s);
+void launch_arm_full(const KParams &p, int32_t mode, uint32_t eval_left, int restore_eps, double eps0,
+                     hipStream_t s);
+void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s);
+void launch_apply(const KParams &p, int specials, hipStream_t s);
+void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);
+void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s);
+void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,
+                    uint32_t n, hipStream_t s);
+
+}  // namespace rlamd

@@ -1,0 +1,201 @@
+// rl_misc.hip — the small kernels around the fused step kernel: lane init
+// (BlackJackEnv::new's deal included), train()/evaluate() arming, the group
+// merge apply, the batched Env trait kernels and device KAT probes.
+#include "rl_train_impl.h"
+
+namespace rlamd {
+
+train_launch_fn train_table_frozen_lake(int, int, int, int);
+train_launch_fn train_table_cliff_walking(int, int, int, int);
+train_launch_fn train_table_taxi(int, int, int, int);
+train_launch_fn train_table_blackjack(int, int, int, int);
+
+train_launch_fn lookup_train(int env, int agent, int policy, int sel, int priv) {
+    switch (env) {
+    case RL_ENV_FROZEN_LAKE: return train_table_frozen_lake(agent, policy, sel, priv);
+    case RL_ENV_CLIFF_WALKING: return train_table_cliff_walking(agent, policy, sel, priv);
+    case RL_ENV_TAXI: return train_table_taxi(agent, policy, sel, priv);
+    case RL_ENV_BLACKJACK: return train_table_blackjack(agent, policy, sel, priv);
+    }
+    return nullptr;
+}
+size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start) {
+    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, agent == RL_AGENT_TRACES, S,
+                       A, n_start, 1).total;
+}
+
+// ---------------------------------------------------------------- lane init
+// Fresh lanes: RNG keyed (seed, global lane), need_reset, DoubleTabularPolicy
+// flag = true, epsilon = eps0.  Blackjack consumes BlackJackEnv::new()'s deal
+// (blackjack.rs:32-46) so the stream matches a freshly constructed reference env.
+__global__ void k_lane_init(KParams p, int env, uint64_t seed, uint64_t lane_offset, double eps0) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    const uint4 r0 = rng_seed(seed, lane_offset + lane);
+    Rng r{r0.x, r0.y, r0.z, r0.w};
+    uint32_t z = 0;
+    if (env == RL_ENV_BLACKJACK) z = EnvDev<RL_ENV_BLACKJACK>::deal(r);
+    p.core[lane] = make_uint4(0, LF_NEED_RESET | LF_DFLAG | ((uint32_t)RL_MODE_TRAIN << LF_MODE_SHIFT), z, 0);
+    p.rng[lane] = make_uint4(r.s0, r.s1, r.s2, r.s3);
+    const uint64_t e = (uint64_t)__double_as_longlong(eps0);
+    p.aux[lane] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), 0, 0);
+    p.epi_reward[lane] = 0.0;
+}
+void launch_lane_init(int env, const KParams &p, uint64_t seed, uint64_t lane_offset, double eps0,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(k_lane_init, dim3((p.L + 255) / 256), dim3(256), 0, s, p, env, seed, lane_offset, eps0);
+}
+
+// ---------------------------------------------------------------- arm
+// start of Agent::train / Agent::evaluate: every lane begins a new episode
+// (src/agent.rs:83 env.reset()), episode counter 0, mode set.  mode < 0 keeps
+// the mode and only restores epsilon (Agent::reset / set_action_selector).
+__global__ void k_arm(KParams p, int32_t mode, uint32_t eval_left, int restore_eps, double eps0) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    uint4 c = p.core[lane];
+    uint4 x = p.aux[lane];
+    if (mode >= 0) {
+        c.y = (c.y & (LF_ACT_MASK | LF_READY | LF_DFLAG)) | LF_NEED_RESET | ((uint32_t)mode << LF_MODE_SHIFT);
+        c.w = 0;
+        x.z = eval_left;
+    }
+    if (restore_eps) {
+        const uint64_t e = (uint64_t)__double_as_longlong(eps0);
+        x.x = (uint32_t)e; x.y = (uint32_t)(e >> 32);
+    }
+    p.core[lane] = c;
+    p.aux[lane] = x;
+}
+void launch_arm_full(const KParams &p, int32_t mode, uint32_t eval_left, int restore_eps, double eps0,
+                     hipStream_t s) {
+    hipLaunchKernelGGL(k_arm, dim3((p.L + 255) / 256), dim3(256), 0, s, p, mode, eval_left, restore_eps, eps0);
+}
+
+__global__ void k_fill_f64(double *ptr, uint64_t n, double v) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ptr[i] = v;
+}
+void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ptr, n, v);
+}
+
+// ---------------------------------------------------------------- merge apply
+// Q_base += Σ_groups ΔQ (already summed by global int64 atomics and, across
+// GPUs, by the caller's all-reduce), then Δ = 0 for the next launch.
+__global__ void k_apply(KParams p, int specials) {
+    const uint32_t PSA = p.P * p.S * p.A, SA = p.S * p.A;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t *d = p.delta;
+    if (i < PSA) {   // Q_base += mean over the groups (and ranks) that changed the entry
+        p.q_base[i] = (int64_t)((uint64_t)p.q_base[i] + (uint64_t)mean_delta(d[i], d[PSA + i]));
+        d[i] = 0;
+        d[PSA + i] = 0;
+        if (specials) {
+            int64_t *fc = d + 2 * PSA + SA + 1;
+            uint32_t f = p.qf_base[i];
+            if (fc[i]) f |= QF_NAN;
+            if (fc[PSA + i]) f |= QF_PINF;
+            if (fc[2 * PSA + i]) f |= QF_NINF;
+            p.qf_base[i] = f;
+            fc[i] = fc[PSA + i] = fc[2 * PSA + i] = 0;
+        }
+    }
+    if (i < SA) {    // UCB counters are counts: summed
+        p.n_base[i] = (uint32_t)((int64_t)p.n_base[i] + d[2 * PSA + i]);
+        d[2 * PSA + i] = 0;
+    }
+    if (i == 0) {
+        p.t_base[0] = (uint64_t)((int64_t)p.t_base[0] + d[2 * PSA + SA]);
+        d[2 * PSA + SA] = 0;
+    }
+}
+void launch_apply(const KParams &p, int specials, hipStream_t s) {
+    const uint32_t PSA = p.P * p.S * p.A;
+    hipLaunchKernelGGL(k_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p, specials);
+}
+
+// ---------------------------------------------------------------- batched Env trait
+template <int ENV>
+__global__ void k_env_reset(KParams p, uint64_t *obs) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward};
+    uint4 c = p.core[lane];
+    const uint4 r0 = p.rng[lane];
+    Rng r{r0.x, r0.y, r0.z, r0.w};
+    c.x = EnvDev<ENV>::reset(c.z, r, t);
+    c.y |= LF_READY;
+    p.core[lane] = c;
+    p.rng[lane] = make_uint4(r.s0, r.s1, r.s2, r.s3);
+    obs[lane] = c.x;
+}
+template <int ENV>
+__global__ void k_env_step(KParams p, const uint32_t *act, uint64_t *obs, double *rew, uint8_t *term) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward};
+    uint4 c = p.core[lane];
+    const uint4 r0 = p.rng[lane];
+    Rng r{r0.x, r0.y, r0.z, r0.w};
+    uint32_t s2 = 0;
+    double rw = 0.0;
+    bool tm = false;
+    uint32_t pos = c.x;
+    EnvDev<ENV>::step(pos, c.z, act[lane], r, t, s2, rw, tm);
+    c.x = s2;
+    if (tm) c.y &= ~LF_READY;
+    p.core[lane] = c;
+    p.rng[lane] = make_uint4(r.s0, r.s1, r.s2, r.s3);
+    obs[lane] = s2;
+    rew[lane] = rw;
+    term[lane] = (uint8_t)tm;
+}
+void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs) {
+    const dim3 g((p.L + 255) / 256), b(256);
+    switch (env) {
+    case RL_ENV_FROZEN_LAKE: hipLaunchKernelGGL(k_env_reset<RL_ENV_FROZEN_LAKE>, g, b, 0, s, p, obs); break;
+    case RL_ENV_CLIFF_WALKING: hipLaunchKernelGGL(k_env_reset<RL_ENV_CLIFF_WALKING>, g, b, 0, s, p, obs); break;
+    case RL_ENV_TAXI: hipLaunchKernelGGL(k_env_reset<RL_ENV_TAXI>, g, b, 0, s, p, obs); break;
+    case RL_ENV_BLACKJACK: hipLaunchKernelGGL(k_env_reset<RL_ENV_BLACKJACK>, g, b, 0, s, p, obs); break;
+    }
+}
+void launch_env_step(int env, const KParams &p, hipStream_t s, const uint32_t *act, uint64_t *obs,
+                     double *rew, uint8_t *term, unsigned int *) {
+    const dim3 g((p.L + 255) / 256), b(256);
+    switch (env) {
+    case RL_ENV_FROZEN_LAKE: hipLaunchKernelGGL(k_env_step<RL_ENV_FROZEN_LAKE>, g, b, 0, s, p, act, obs, rew, term); break;
+    case RL_ENV_CLIFF_WALKING: hipLaunchKernelGGL(k_env_step<RL_ENV_CLIFF_WALKING>, g, b, 0, s, p, act, obs, rew, term); break;
+    case RL_ENV_TAXI: hipLaunchKernelGGL(k_env_step<RL_ENV_TAXI>, g, b, 0, s, p, act, obs, rew, term); break;
+    case RL_ENV_BLACKJACK: hipLaunchKernelGGL(k_env_step<RL_ENV_BLACKJACK>, g, b, 0, s, p, act, obs, rew, term); break;
+    }
+}
+
+// ---------------------------------------------------------------- KAT probes
+__global__ void k_kat_log(const double *x, double *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = rl_log(x[i]);
+}
+__global__ void k_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint4 r0 = rng_seed(seed, lane);
+    Rng r{r0.x, r0.y, r0.z, r0.w};
+    for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
+}
+__global__ void k_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,
+                          uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ucb_value(q[i], c, rl_log((double)t[i]), nc[i]);
+}
+void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_kat_log, dim3((n + 255) / 256), dim3(256), 0, s, x, out, n);
+}
+void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_kat_rng, dim3(1), dim3(64), 0, s, seed, lane, n, out);
+}
+void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,
+                    uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_kat_ucb, dim3((n + 255) / 256), dim3(256), 0, s, q, nc, t, c, out, n);
+}
+
+}  // namespace rlamd

@@ -1,0 +1,639 @@
+// rl_train_impl.h — the fused training-step kernels (included by rl_train_<env>.hip).
+//
+// One thread = one env lane.  A launch runs K = sync_every synchronous steps of
+// Agent::train's loop body (src/agent.rs:86-106) for every lane, entirely in
+// registers / LDS; lane records are read once and written once per launch.
+//
+//  k_train_shared : a workgroup is a learner group of G lanes sharing one Q
+//                   copy in LDS as int64 fixed point (2^-40).  Each step: reads
+//                   against the step-start snapshot, then every lane's delta is
+//                   added with ds_add_u64 (integer: order free, bit-reproducible),
+//                   then the group's ΔQ goes to HBM by global int64 atomics.
+//  k_train_private: group_size == 1.  Every lane is a complete reference agent
+//                   with f64 Q / UCB counters in HBM (SoA [entry][lane]) — the
+//                   reference's arithmetic bit for bit.
+#pragma once
+#include "rl_device.h"
+
+namespace rlamd {
+
+struct SmemLayout {
+    uint32_t q, sum, cnt, qf, n, t, list, tr, cdf, total;
+};
+__host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+// LDS carve of one learner group (shared mode) or of the tables only (private).
+//   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40)
+//   sum  int64 [P][S][A]   this step's summed deltas per entry
+//   cnt  u16   [P][S][A]   this step's contributions per entry (u32-word atomics)
+//   qf   u8    [P][S][A]   sticky non-finite flags (UCB + expected SARSA only)
+//   n/t  UCB counters;  list u16 touched entries + count (traces);  tr/cdf env tables
+__host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int traces, uint32_t S,
+                                                  uint32_t A, uint32_t n_start, int shared_q) {
+    SmemLayout l;
+    const uint32_t SA = S * A, PSA = (uint32_t)P * SA;
+    uint32_t off = 0;
+    l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
+    l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
+    l.cnt = off; off += shared_q ? align16(((PSA + 1u) / 2u) * 4u) : 0u;
+    l.qf = off; off += (shared_q && ucb) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
+    l.n = off; off += (shared_q && ucb) ? align16(SA * 4u) : 0u;
+    l.t = off; off += (shared_q && ucb) ? 16u : 0u;
+    l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
+    l.tr = off; off += env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
+    l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_TAXI) ? align16(n_start * 8u) : 0u;
+    l.total = off;
+    return l;
+}
+
+// The shared-mode combination rule (oracle: rlref.c mean_delta): an entry moves
+// by the MEAN of the n contributions it received; n == 1 is exact, n > 1 is an
+// f64 divide + truncation (correctly rounded on host and gfx950 alike).
+__host__ __device__ inline int64_t mean_delta(int64_t sum, int64_t n) {
+    if (n <= 1) return n == 1 ? sum : 0;
+    return (int64_t)__builtin_trunc((double)sum / (double)n);
+}
+
+// ---------------------------------------------------------------- lane state
+struct LaneRegs {
+    Rng rng;
+    uint32_t s, a, z, train_ep, eval_left, epi_len;
+    uint32_t mode;
+    bool need_reset, ready, dflag;
+    double eps, epi_reward;
+    // per-launch counters
+    uint32_t n_train, n_eval, n_tep, n_eep;
+    int64_t rsum;
+};
+
+__device__ __forceinline__ void lane_load(const KParams &p, uint64_t lane, bool active, LaneRegs &L) {
+    uint4 c = make_uint4(0, 0, 0, 0), r = make_uint4(1, 0, 0, 0), x = make_uint4(0, 0, 0, 0);
+    double er = 0.0;
+    if (active) { c = p.core[lane]; r = p.rng[lane]; x = p.aux[lane]; er = p.epi_reward[lane]; }
+    L.rng.s0 = r.x; L.rng.s1 = r.y; L.rng.s2 = r.z; L.rng.s3 = r.w;
+    L.s = c.x;
+    L.a = c.y & LF_ACT_MASK;
+    L.need_reset = (c.y & LF_NEED_RESET) != 0;
+    L.ready = (c.y & LF_READY) != 0;
+    L.dflag = (c.y & LF_DFLAG) != 0;
+    L.mode = active ? (c.y >> LF_MODE_SHIFT) & 3u : (uint32_t)RL_MODE_DONE;
+    L.z = c.z;
+    L.train_ep = c.w;
+    L.eps = __longlong_as_double((long long)(((uint64_t)x.y << 32) | x.x));
+    L.eval_left = x.z;
+    L.epi_len = x.w;
+    L.epi_reward = er;
+    L.n_train = L.n_eval = L.n_tep = L.n_eep = 0;
+    L.rsum = 0;
+}
+__device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, const LaneRegs &L) {
+    const uint32_t y = (L.a & LF_ACT_MASK) | (L.need_reset ? LF_NEED_RESET : 0u) |
+                       (L.ready ? LF_READY : 0u) | (L.dflag ? LF_DFLAG : 0u) |
+                       (L.mode << LF_MODE_SHIFT);
+    p.core[lane] = make_uint4(L.s, y, L.z, L.train_ep);
+    p.rng[lane] = make_uint4(L.rng.s0, L.rng.s1, L.rng.s2, L.rng.s3);
+    const uint64_t e = (uint64_t)__double_as_longlong(L.eps);
+    p.aux[lane] = make_uint4((uint32_t)e, (uint32_t)(e >> 32), L.eval_left, L.epi_len);
+    p.epi_reward[lane] = L.epi_reward;
+}
+
+// per-launch counters -> rl_stats (one atomic per wave per counter)
+__device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, bool active) {
+    const uint64_t v[6] = {L.n_train, L.n_eval, L.n_tep, L.n_eep, (uint64_t)L.rsum,
+                           (uint64_t)(active && L.mode == RL_MODE_DONE)};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int64_t s = wave_sum_i64((int64_t)v[i]);
+        if ((threadIdx.x & 63u) == 0 && s != 0) atomicAdd(&p.stats[i], (unsigned long long)s);
+    }
+}
+
+// bookkeeping after the update: src/agent.rs:98-116 + the eval interleave.
+// Written as predicated selects (no divergent branches): lanes end episodes at
+// different steps, and the branchy form was mis-scheduled at -O3 (a lost
+// train_ep increment, caught by the parity tests).
+__device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32_t s2, uint32_t a2,
+                                           double r, bool term) {
+    L.epi_reward += r;
+    L.epi_len += 1;
+    L.s = s2;
+    L.a = a2;
+    const bool tr = term && L.mode == RL_MODE_TRAIN;
+    const bool ev = term && L.mode == RL_MODE_EVAL;
+    const uint32_t ep = L.train_ep;                      // index of the episode that just ended
+    const uint32_t new_ep = ep + (tr ? 1u : 0u);
+    bool hit = false;                                    // episode % eval_at == 0 (src/agent.rs:107)
+    if (p.eval_at) hit = ((uint64_t)ep % p.eval_at) == 0;
+    const bool go_eval = tr && hit && p.eval_episodes != 0;
+    const bool reached = p.target_episodes != 0 && (uint64_t)new_ep >= p.target_episodes;
+    const bool tr_done = tr && !go_eval && reached;
+    const uint32_t el = L.eval_left - (ev ? 1u : 0u);
+    const bool ev_end = ev && el == 0u;
+    const bool ev_fin = p.eval_only != 0 || reached;
+    uint32_t mode = L.mode;
+    mode = go_eval ? (uint32_t)RL_MODE_EVAL : mode;
+    mode = tr_done ? (uint32_t)RL_MODE_DONE : mode;
+    mode = ev_end ? (ev_fin ? (uint32_t)RL_MODE_DONE : (uint32_t)RL_MODE_TRAIN) : mode;
+    L.mode = mode;
+    L.train_ep = new_ep;
+    L.eval_left = go_eval ? p.eval_episodes : el;
+    L.need_reset = L.need_reset || term;
+    L.n_tep += tr ? 1u : 0u;
+    L.n_eep += ev ? 1u : 0u;
+    L.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;
+}
+
+__device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint64_t lane,
+                                             const LaneRegs &L, bool alive, uint32_t s2, uint32_t a2,
+                                             double r, bool term, double td, uint32_t mode_before) {
+    rl_step_record rec;
+    rec.s = alive ? L.s : 0u;
+    rec.s2 = s2;
+    rec.a = (uint8_t)(alive ? L.a : 0u);
+    rec.a2 = (uint8_t)a2;
+    rec.term = (uint8_t)term;
+    rec.mode = (uint8_t)mode_before;
+    rec.pad = 0;
+    rec.r = r;
+    rec.td = td;
+    p.rec[(uint64_t)k * p.L + lane] = rec;
+}
+
+// ======================================================================== shared
+template <int ENV, int AGENT, int POLICY, int SEL>
+__global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
+    using E = EnvDev<ENV>;
+    constexpr int A = E::A;
+    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    constexpr bool UCB = SEL == RL_SEL_UCB;
+    const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
+    const bool spec = UCB && p.algo == RL_ALGO_EXPECTED_SARSA;   // inf/NaN possible
+
+    constexpr bool TRACES = AGENT == RL_AGENT_TRACES;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES, S, A, p.n_start, 1);
+    unsigned long long *Q = (unsigned long long *)(smem + lay.q);
+    unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
+    uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // two u16 counters per word
+    uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
+    uint32_t *QF = (uint32_t *)(smem + lay.qf);          // four u8 flag sets per word
+    uint8_t *QF8 = (uint8_t *)(smem + lay.qf);
+    uint32_t *N = (uint32_t *)(smem + lay.n);
+    unsigned long long *T = (unsigned long long *)(smem + lay.t);
+    uint16_t *LIST = (uint16_t *)(smem + lay.list);
+    uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSA * 2u));
+    uint32_t *TR = (uint32_t *)(smem + lay.tr);
+    double *CDF = (double *)(smem + lay.cdf);
+
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    for (uint32_t i = tid; i < PSA; i += nthr) { Q[i] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
+    for (uint32_t i = tid; i < (PSA + 1u) / 2u; i += nthr) CNT[i] = 0u;
+    if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
+    if constexpr (UCB) {
+        for (uint32_t i = tid; i < PSA; i += nthr) QF8[i] = (uint8_t)p.qf_base[i];
+        for (uint32_t i = tid; i < SA; i += nthr) N[i] = p.n_base[i];
+        if (tid == 0) T[0] = p.t_base[0];
+    }
+    if constexpr (ENV != RL_ENV_BLACKJACK)
+        for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
+    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_TAXI)
+        for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
+    __syncthreads();
+
+    EnvTables tabs;
+    tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+
+    const uint64_t lane = (uint64_t)blockIdx.x * p.G + tid;
+    const bool active = tid < p.G && lane < p.L;
+    LaneRegs L;
+    lane_load(p, lane, active, L);
+
+    auto qv = [&](uint32_t idx) -> double {
+        const int64_t raw = (int64_t)Q[idx];
+        if constexpr (UCB) { if (spec) return q_val(raw, QF8[idx]); }
+        return q_val(raw);
+    };
+    // add one contribution set (sum of n deltas) to entry idx; returns true for
+    // the first contributor of the step (the entry's owner for the apply phase)
+    auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
+        const uint32_t sh = (idx & 1u) * 16u;
+        const uint32_t old = atomicAdd(&CNT[idx >> 1], n << sh);
+        if (sum) atomicAdd(&SUM[idx], (unsigned long long)sum);
+        if constexpr (UCB) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
+        return ((old >> sh) & 0xffffu) == 0u;
+    };
+    // owner: Q[idx] += mean of the step's contributions, then clear the accumulators
+    auto settle = [&](uint32_t idx) {
+        const uint32_t n = CNT16[idx];
+        const int64_t sum = (int64_t)SUM[idx];
+        Q[idx] = Q[idx] + (unsigned long long)mean_delta(sum, (int64_t)n);
+        SUM[idx] = 0ull;
+        CNT16[idx] = 0;
+    };
+    // Policy::predict (tabular_policy.rs:27-29; double_tabular_policy.rs:31-40)
+    auto predict = [&](uint32_t s, double (&v)[A]) {
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+            if constexpr (P == 1) v[i] = qv(s * A + i);
+            else v[i] = (qv(s * A + i) + qv(SA + s * A + i)) / 2.0;
+        }
+    };
+    // Agent::get_action against the snapshot (UCB increments applied by the caller)
+    auto select = [&](uint32_t s) -> uint32_t {
+        double v[A];
+        predict(s, v);
+        if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
+            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
+            return argmax<A>(v);
+        } else {                                    // upper_confidence_bound.rs:29-42
+            const double lnt = rl_log((double)T[0]);
+            double u[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)N[s * A + i]);
+            return argmax<A>(u);
+        }
+    };
+
+    for (uint32_t k = 0; k < p.K; ++k) {
+        // ---------------- R-phase: env.reset() + get_action (src/agent.rs:83-84)
+        const bool doR = L.mode != RL_MODE_DONE && L.need_reset;
+        if (doR) {
+            L.s = E::reset(L.z, L.rng, tabs);
+            L.ready = true;
+            L.a = select(L.s);
+            L.need_reset = false;
+            L.epi_reward = 0.0;
+            L.epi_len = 0;
+        }
+        if constexpr (UCB) {
+            if (__syncthreads_or(doR)) {
+                if (doR) atomicAdd(&N[L.s * A + L.a], 1u);
+                const uint32_t c = (uint32_t)__popcll(__ballot(doR));
+                if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
+                __syncthreads();
+            }
+        }
+        // ---------------- S-phase: step + next action (src/agent.rs:88-89)
+        const bool alive = L.mode != RL_MODE_DONE;
+        const uint32_t mode_before = L.mode;
+        uint32_t s2 = 0, a2 = 0;
+        double r = 0.0;
+        bool term = false;
+        if (alive) {
+            uint32_t pos = L.s;
+            E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
+            if (term) L.ready = false;
+            a2 = select(s2);
+        }
+        if constexpr (UCB) {
+            __syncthreads();
+            if (alive) atomicAdd(&N[s2 * A + a2], 1u);
+            const uint32_t c = (uint32_t)__popcll(__ballot(alive));
+            if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
+            __syncthreads();
+        }
+        // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
+        const bool train = alive && L.mode == RL_MODE_TRAIN;
+        const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;   // get_values: flag ? alpha : beta
+        const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;    // update:     flag ? beta : alpha
+        double td = 0.0;
+        int64_t dq = 0;
+        uint32_t dfl = 0;
+        if (train) {
+            double q2[A], pr[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) { q2[i] = qv(vt * SA + s2 * A + i); pr[i] = 0.0; }
+            if (p.algo == RL_ALGO_EXPECTED_SARSA) {
+                if constexpr (!UCB) {
+                    eps_probs<A>(L.eps, q2, pr);
+                } else {                                   // upper_confidence_bound.rs:48-63
+                    const double lnt = rl_log((double)T[0]);
+                    double sum = 0.0;
+#pragma unroll
+                    for (int i = 0; i < A; ++i) {
+                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)N[s2 * A + i]);
+                        sum += pr[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < A; ++i) pr[i] /= sum;
+                }
+            }
+            const double fq = future_q<A>(p.algo, q2, a2, pr);
+            const double qa = qv(vt * SA + L.s * A + L.a);
+            td = r + p.gamma * fq - qa;
+            if constexpr (AGENT == RL_AGENT_ONE_STEP) dq = q_fix(p.lr * td, dfl);
+        }
+        __syncthreads();   // every Q read of this step happened before any write
+        if constexpr (AGENT == RL_AGENT_ONE_STEP) {
+            const uint32_t idx = ut * SA + L.s * A + L.a;
+            bool owner = false;
+            if (train) owner = contribute(idx, dq, 1u, dfl);
+            __syncthreads();   // all contributions in
+            if (owner) settle(idx);
+        } else {
+            // accumulating trace: E[s][a] += 1, then for every visited (o, b):
+            // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda.  Per-lane deltas
+            // are summed exactly across the wave, one ds_add_u64 per entry.
+            const uint64_t Ls = p.L;
+            if (train) {
+                double *e = &p.trace[(uint64_t)(L.s * A + L.a) * Ls + lane];
+                *e = *e + 1.0;
+                p.visited[(uint64_t)(L.s >> 5) * Ls + lane] |= 1u << (L.s & 31u);
+            }
+            for (uint32_t w = 0; w < p.vis_words; ++w) {
+                const uint32_t mine = train ? p.visited[(uint64_t)w * Ls + lane] : 0u;
+                uint32_t uw = wave_or_u32(mine);
+                while (uw) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(uw);
+                    uw &= uw - 1u;
+                    const uint32_t o = w * 32u + bit;
+                    const bool has = (mine >> bit) & 1u;
+#pragma unroll
+                    for (int b = 0; b < A; ++b) {
+                        int64_t d = 0;
+                        uint32_t fl = 0;
+                        if (has) {
+                            double *ep = &p.trace[(uint64_t)(o * A + b) * Ls + lane];
+                            const double ev = *ep;
+                            d = q_fix(p.lr * (td * ev), fl);
+                            *ep = ev * p.gl;
+                        }
+#pragma unroll
+                        for (int t = 0; t < P; ++t) {
+                            const bool mine_t = has && ut == (uint32_t)t;
+                            const int64_t sum = wave_sum_i64(mine_t ? d : 0);
+                            const uint32_t n = (uint32_t)__popcll(__ballot(mine_t));
+                            uint32_t f = 0;
+                            if constexpr (UCB) f = wave_or_u32(mine_t ? fl : 0u);
+                            const uint32_t idx = (uint32_t)t * SA + o * A + b;
+                            if ((tid & 63u) == 0 && n) {
+                                if (contribute(idx, sum, n, f)) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
+                            }
+                        }
+                    }
+                }
+            }
+            if (train && term) {                          // trace map cleared on termination
+                for (uint32_t w = 0; w < p.vis_words; ++w) {
+                    uint32_t m = p.visited[(uint64_t)w * Ls + lane];
+                    while (m) {
+                        const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+#pragma unroll
+                        for (int b = 0; b < A; ++b) p.trace[(uint64_t)(o * A + b) * Ls + lane] = 0.0;
+                    }
+                    p.visited[(uint64_t)w * Ls + lane] = 0u;
+                }
+            }
+            __syncthreads();   // all contributions in
+            const uint32_t n_touched = LISTN[0];
+            for (uint32_t i = tid; i < n_touched; i += nthr) settle(LIST[i]);
+            __syncthreads();
+            if (tid == 0) LISTN[0] = 0u;
+        }
+        __syncthreads();   // Q_{t+1} complete before the next step's reads
+        if (alive) {
+            if (train) {
+                if (P == 2) L.dflag = !L.dflag;            // after_update
+                if (term) { if constexpr (!UCB) L.eps = decay_eps(p, L.eps); }
+                L.n_train++;
+            } else {
+                L.n_eval++;
+            }
+            if (p.rec) write_record(p, k, lane, L, true, s2, a2, r, term, td, mode_before);
+            after_step(p, L, s2, a2, r, term);
+        } else if (p.rec && active) {
+            write_record(p, k, lane, L, false, 0, 0, 0.0, false, 0.0, RL_MODE_DONE);
+        }
+    }
+
+    if (active) lane_store(p, lane, L);
+    flush_stats(p, L, active);
+
+    // ---------------- emit this group's ΔQ (and ΔN, Δt, new flags) for the merge
+    __syncthreads();
+    // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts]
+    for (uint32_t i = tid; i < PSA; i += nthr) {
+        const int64_t d = (int64_t)(Q[i] - (unsigned long long)p.q_base[i]);
+        if (d) {
+            atomicAdd((unsigned long long *)&p.delta[i], (unsigned long long)d);
+            atomicAdd((unsigned long long *)&p.delta[PSA + i], 1ull);
+        }
+    }
+    if constexpr (UCB) {
+        for (uint32_t i = tid; i < SA; i += nthr) {
+            const int64_t d = (int64_t)N[i] - (int64_t)p.n_base[i];
+            if (d) atomicAdd((unsigned long long *)&p.delta[2 * PSA + i], (unsigned long long)d);
+        }
+        if (tid == 0) {
+            const int64_t d = (int64_t)(T[0] - p.t_base[0]);
+            if (d) atomicAdd((unsigned long long *)&p.delta[2 * PSA + SA], (unsigned long long)d);
+        }
+        if (spec) {
+            int64_t *fc = p.delta + 2 * PSA + SA + 1;
+            for (uint32_t i = tid; i < PSA; i += nthr) {
+                const uint32_t nf = QF8[i] & ~p.qf_base[i];
+                if (nf & QF_NAN) atomicAdd((unsigned long long *)&fc[i], 1ull);
+                if (nf & QF_PINF) atomicAdd((unsigned long long *)&fc[PSA + i], 1ull);
+                if (nf & QF_NINF) atomicAdd((unsigned long long *)&fc[2 * PSA + i], 1ull);
+            }
+        }
+    }
+}
+
+// ======================================================================== private
+template <int ENV, int AGENT, int POLICY, int SEL>
+__global__ void __launch_bounds__(256) k_train_private(KParams p) {
+    using E = EnvDev<ENV>;
+    constexpr int A = E::A;
+    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    constexpr bool UCB = SEL == RL_SEL_UCB;
+    const uint32_t S = p.S, SA = S * (uint32_t)A;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES, S, A, p.n_start, 0);
+    uint32_t *TR = (uint32_t *)(smem + lay.tr);
+    double *CDF = (double *)(smem + lay.cdf);
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    if constexpr (ENV != RL_ENV_BLACKJACK)
+        for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
+    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_TAXI)
+        for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
+    __syncthreads();
+
+    EnvTables tabs;
+    tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+
+    const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
+    const bool active = lane < p.L;
+    if (!active) return;
+    LaneRegs L;
+    lane_load(p, lane, true, L);
+    const uint64_t Ls = p.L;
+    uint64_t t = UCB ? p.t_priv[lane] : 0;
+
+    auto qref = [&](uint32_t idx) -> double & { return p.q_priv[(uint64_t)idx * Ls + lane]; };
+    auto predict = [&](uint32_t s, double (&v)[A]) {
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+            if constexpr (P == 1) v[i] = qref(s * A + i);
+            else v[i] = (qref(s * A + i) + qref(SA + s * A + i)) / 2.0;
+        }
+    };
+    // get_action with the reference's immediate UCB increments
+    auto select = [&](uint32_t s) -> uint32_t {
+        double v[A];
+        predict(s, v);
+        if constexpr (!UCB) {
+            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
+            return argmax<A>(v);
+        } else {
+            const double lnt = rl_log((double)t);
+            double u[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i)
+                u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)p.n_priv[(uint64_t)(s * A + i) * Ls + lane]);
+            const uint32_t a = argmax<A>(u);
+            p.n_priv[(uint64_t)(s * A + a) * Ls + lane] += 1u;
+            t += 1;
+            return a;
+        }
+    };
+
+    for (uint32_t k = 0; k < p.K; ++k) {
+        if (L.mode != RL_MODE_DONE && L.need_reset) {
+            L.s = E::reset(L.z, L.rng, tabs);
+            L.ready = true;
+            L.a = select(L.s);
+            L.need_reset = false;
+            L.epi_reward = 0.0;
+            L.epi_len = 0;
+        }
+        if (L.mode == RL_MODE_DONE) {
+            if (p.rec) write_record(p, k, lane, L, false, 0, 0, 0.0, false, 0.0, RL_MODE_DONE);
+            continue;
+        }
+        const uint32_t mode_before = L.mode;
+        uint32_t s2 = 0;
+        double r = 0.0;
+        bool term = false;
+        {
+            uint32_t pos = L.s;
+            E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
+            if (term) L.ready = false;
+        }
+        const uint32_t a2 = select(s2);
+        double td = 0.0;
+        if (L.mode == RL_MODE_TRAIN) {
+            const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;
+            const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;
+            double q2[A], pr[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) { q2[i] = qref(vt * SA + s2 * A + i); pr[i] = 0.0; }
+            if (p.algo == RL_ALGO_EXPECTED_SARSA) {
+                if constexpr (!UCB) {
+                    eps_probs<A>(L.eps, q2, pr);
+                } else {
+                    const double lnt = rl_log((double)t);
+                    double sum = 0.0;
+#pragma unroll
+                    for (int i = 0; i < A; ++i) {
+                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt,
+                                          (double)p.n_priv[(uint64_t)(s2 * A + i) * Ls + lane]);
+                        sum += pr[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < A; ++i) pr[i] /= sum;
+                }
+            }
+            const double fq = future_q<A>(p.algo, q2, a2, pr);
+            const double qa = qref(vt * SA + L.s * A + L.a);
+            td = r + p.gamma * fq - qa;
+            if constexpr (AGENT == RL_AGENT_ONE_STEP) {
+                double &q = qref(ut * SA + L.s * A + L.a);     // tabular_policy.rs:36
+                q = q + p.lr * td;
+            } else {
+                double *e0 = &p.trace[(uint64_t)(L.s * A + L.a) * Ls + lane];
+                *e0 = *e0 + 1.0;
+                p.visited[(uint64_t)(L.s >> 5) * Ls + lane] |= 1u << (L.s & 31u);
+                for (uint32_t w = 0; w < p.vis_words; ++w) {
+                    uint32_t m = p.visited[(uint64_t)w * Ls + lane];
+                    while (m) {
+                        const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+#pragma unroll
+                        for (int b = 0; b < A; ++b) {
+                            double *ep = &p.trace[(uint64_t)(o * A + b) * Ls + lane];
+                            const double ev = *ep;
+                            double &q = qref(ut * SA + o * A + b);
+                            q = q + p.lr * (td * ev);
+                            *ep = ev * p.gl;
+                        }
+                    }
+                }
+                if (term) {
+                    for (uint32_t w = 0; w < p.vis_words; ++w) {
+                        uint32_t m = p.visited[(uint64_t)w * Ls + lane];
+                        while (m) {
+                            const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
+                            m &= m - 1u;
+#pragma unroll
+                            for (int b = 0; b < A; ++b) p.trace[(uint64_t)(o * A + b) * Ls + lane] = 0.0;
+                        }
+                        p.visited[(uint64_t)w * Ls + lane] = 0u;
+                    }
+                }
+            }
+            if (P == 2) L.dflag = !L.dflag;
+            if (term) { if constexpr (!UCB) L.eps = decay_eps(p, L.eps); }
+            L.n_train++;
+        } else {
+            L.n_eval++;
+        }
+        if (p.rec) write_record(p, k, lane, L, true, s2, a2, r, term, td, mode_before);
+        after_step(p, L, s2, a2, r, term);
+    }
+    lane_store(p, lane, L);
+    if (UCB) p.t_priv[lane] = t;
+    // stats without wave reductions (inactive lanes returned early)
+    const uint64_t v[6] = {L.n_train, L.n_eval, L.n_tep, L.n_eep, (uint64_t)L.rsum,
+                           (uint64_t)(L.mode == RL_MODE_DONE)};
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+        if (v[i]) atomicAdd(&p.stats[i], (unsigned long long)v[i]);
+}
+
+// ---------------------------------------------------------------- launch table
+template <int ENV, int AGENT, int POLICY, int SEL, int PRIV>
+hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream) {
+    const void *k = PRIV ? (const void *)k_train_private<ENV, AGENT, POLICY, SEL>
+                         : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL>;
+    if (smem > 64 * 1024) {   // gfx950: a workgroup may use up to the CU's 160 KiB of LDS
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    if constexpr (PRIV)
+        hipLaunchKernelGGL((k_train_private<ENV, AGENT, POLICY, SEL>), grid, block, smem, stream, p);
+    else
+        hipLaunchKernelGGL((k_train_shared<ENV, AGENT, POLICY, SEL>), grid, block, smem, stream, p);
+    return hipGetLastError();
+}
+
+template <int ENV>
+train_launch_fn train_table_entry(int agent, int policy, int sel, int priv) {
+#define RLAMD_E(AG, PO, SE, PR)                                                                    \
+    if (agent == AG && policy == PO && sel == SE && priv == PR) return &launch_train<ENV, AG, PO, SE, PR>;
+#define RLAMD_E2(AG, PO, SE) RLAMD_E(AG, PO, SE, 0) RLAMD_E(AG, PO, SE, 1)
+#define RLAMD_E3(AG, PO) RLAMD_E2(AG, PO, RL_SEL_EPS_GREEDY) RLAMD_E2(AG, PO, RL_SEL_UCB)
+#define RLAMD_E4(AG) RLAMD_E3(AG, RL_POLICY_TABULAR) RLAMD_E3(AG, RL_POLICY_DOUBLE)
+    RLAMD_E4(RL_AGENT_ONE_STEP)
+    RLAMD_E4(RL_AGENT_TRACES)
+#undef RLAMD_E4
+#undef RLAMD_E3
+#undef RLAMD_E2
+#undef RLAMD_E
+    return nullptr;
+}
+
+}  // namespace rlamd

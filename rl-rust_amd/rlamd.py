@@ -1,0 +1,386 @@
+"""ctypes binding to librlamd.so (include/rl.h) for tests and bench.py.
+
+This is plumbing over the C ABI, shaped like the reference's Rust traits
+(src/env.rs:19-49 Env, src/agent.rs:47-164 Agent).  All compute runs in the
+gfx950 kernels of librlamd.so; there is no CPU fallback: if the library or a
+GPU is missing, every compute call raises RLError.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.environ.get("RLAMD_LIB", os.path.join(HERE, "lib", "librlamd.so"))
+INCLUDE_H = os.path.join(ROOT, "include", "rl.h")
+
+ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}
+AGENT = {"one_step": 0, "traces": 1}
+POLICY = {"tabular": 0, "double": 1}
+SELECTOR = {"eps_greedy": 0, "ucb": 1}
+ALGO = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}
+RL_OK, RL_E_NOT_READY = 0, 1
+
+
+class RLError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rl error {code}: {msg}")
+        self.code = code
+
+
+class EnvConfig(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("map8x8", C.c_int32), ("slippery", C.c_int32),
+                ("max_steps", C.c_uint32)]
+
+
+class AgentConfig(C.Structure):
+    _fields_ = [
+        ("env", EnvConfig),
+        ("agent", C.c_int32), ("policy", C.c_int32), ("selector", C.c_int32),
+        ("algo", C.c_int32), ("decay_kind", C.c_int32),
+        ("lr", C.c_double), ("gamma", C.c_double), ("lambda_", C.c_double),
+        ("eps0", C.c_double), ("eps_decay", C.c_double), ("eps_final", C.c_double),
+        ("ucb_c", C.c_double), ("q_default", C.c_double),
+        ("seed", C.c_uint64), ("lane_offset", C.c_uint64),
+        ("n_lanes", C.c_uint32), ("group_size", C.c_uint32), ("sync_every", C.c_uint32),
+        ("eval_episodes", C.c_uint32), ("device", C.c_int32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [("train_steps", C.c_uint64), ("eval_steps", C.c_uint64),
+                ("train_episodes", C.c_uint64), ("eval_episodes", C.c_uint64),
+                ("reward_sum_q16", C.c_int64), ("done_lanes", C.c_uint64),
+                ("launches", C.c_uint64), ("reserved", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
+                         ("term", "u1"), ("mode", "u1"), ("pad", "<u4"),
+                         ("r", "<f8"), ("td", "<f8")])
+
+# every function include/rl.h declares: name -> (restype, argtypes)
+_P = C.POINTER
+_V = C.c_void_p
+SIGNATURES = {
+    "rl_last_error": (C.c_char_p, []),
+    "rl_abi_version": (C.c_int, []),
+    "rl_device_count": (C.c_int, [_P(C.c_int)]),
+    "rl_blackjack_obs_id": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "rl_obs_to_reference": (C.c_uint64, [C.c_int32, C.c_uint32]),
+    "rl_env_dims": (C.c_int, [_P(EnvConfig), _P(C.c_uint32), _P(C.c_uint32)]),
+    "rl_env_table": (C.c_int, [_P(EnvConfig), _V, _V, _V, _V, _V]),
+    "rl_env_create": (C.c_int, [_P(EnvConfig), C.c_uint32, C.c_uint64, C.c_uint64, C.c_int32, _P(_V)]),
+    "rl_env_destroy": (None, [_V]),
+    "rl_env_reset": (C.c_int, [_V, _V]),
+    "rl_env_step": (C.c_int, [_V, _V, _V, _V, _V]),
+    "rl_agent_create": (C.c_int, [_P(AgentConfig), _P(_V)]),
+    "rl_agent_destroy": (None, [_V]),
+    "rl_agent_set_future_q_value_func": (C.c_int, [_V, C.c_int32]),
+    "rl_agent_set_action_selector": (C.c_int, [_V, C.c_int32, C.c_double, C.c_double, C.c_double,
+                                               C.c_int32, C.c_double]),
+    "rl_agent_reset": (C.c_int, [_V]),
+    "rl_agent_train": (C.c_int, [_V, C.c_uint64, C.c_uint64, _P(Stats)]),
+    "rl_agent_evaluate": (C.c_int, [_V, C.c_uint64, _P(Stats)]),
+    "rl_agent_run": (C.c_int, [_V, C.c_uint32]),
+    "rl_agent_synchronize": (C.c_int, [_V]),
+    "rl_agent_stats": (C.c_int, [_V, _P(Stats)]),
+    "rl_agent_get_q": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_set_q": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_get_q_raw": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_get_ucb": (C.c_int, [_V, _V, C.c_size_t, _V, C.c_size_t]),
+    "rl_agent_get_epsilon": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_set_recording": (C.c_int, [_V, C.c_int32]),
+    "rl_agent_take_records": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64)]),
+    "rl_agent_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
+    "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
+    "rl_agent_delta_words": (C.c_int, [_V, _P(C.c_uint64)]),
+    "rl_agent_set_delta_buffer": (C.c_int, [_V, _V, C.c_uint64]),
+    "rl_agent_launch_train": (C.c_int, [_V]),
+    "rl_agent_launch_apply": (C.c_int, [_V]),
+    "rl_agent_set_stream": (C.c_int, [_V, _V]),
+    "rl_agent_set_timing": (C.c_int, [_V, C.c_int32]),
+    "rl_agent_get_timing": (C.c_int, [_V, _P(C.c_double), _P(C.c_uint64)]),
+    "rl_kat_log": (C.c_int, [C.c_int32, _V, _V, C.c_uint32]),
+    "rl_kat_rng": (C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint32, _V]),
+    "rl_kat_ucb": (C.c_int, [C.c_int32, _V, _V, _V, C.c_double, _V, C.c_uint32]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load librlamd.so (fails loudly if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RLError(-1, f"{LIB_PATH} missing: build the HIP extension first (make -C rl-rust_amd)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != RL_OK:
+        raise RLError(rc, lib().rl_last_error().decode())
+
+
+def env_config(p):
+    c = EnvConfig()
+    c.kind = ENV[p["env"]] if isinstance(p["env"], str) else p["env"]
+    c.map8x8, c.slippery, c.max_steps = p.get("map8x8", 0), p.get("slippery", 0), p.get("max_steps", 100)
+    return c
+
+
+def default_params(**kw):
+    """Reference CLI defaults (src/bin/frozen_lake.rs:35-73; decay rule :84)."""
+    p = dict(env="frozen_lake", map8x8=0, slippery=0, max_steps=100, agent="one_step",
+             policy="tabular", selector="eps_greedy", algo="qlearning", decay_kind=0,
+             lr=0.05, gamma=0.95, lambda_=0.5, eps0=1.0, n_episodes_for_decay=100000,
+             exploration_time=0.5, eps_final=0.0, ucb_c=0.5, q_default=0.0, seed=0x5EED,
+             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100, device=0)
+    p.update(kw)
+    if "eps_decay" not in p:
+        p["eps_decay"] = p["eps0"] / (p["exploration_time"] * p["n_episodes_for_decay"])
+    return p
+
+
+def agent_config(p):
+    c = AgentConfig()
+    c.env = env_config(p)
+    c.agent = AGENT[p["agent"]] if isinstance(p["agent"], str) else p["agent"]
+    c.policy = POLICY[p["policy"]] if isinstance(p["policy"], str) else p["policy"]
+    c.selector = SELECTOR[p["selector"]] if isinstance(p["selector"], str) else p["selector"]
+    c.algo = ALGO[p["algo"]] if isinstance(p["algo"], str) else p["algo"]
+    c.decay_kind = p["decay_kind"]
+    for k in ("lr", "gamma", "lambda_", "eps0", "eps_decay", "eps_final", "ucb_c", "q_default"):
+        setattr(c, k, float(p[k]))
+    c.seed, c.lane_offset = p["seed"], p["lane_offset"]
+    c.n_lanes, c.group_size, c.sync_every = p["n_lanes"], p["group_size"], p["sync_every"]
+    c.eval_episodes, c.device = p["eval_episodes"], p["device"]
+    return c
+
+
+def env_dims(p):
+    c = env_config(p)
+    S, A = C.c_uint32(), C.c_uint32()
+    check(lib().rl_env_dims(C.byref(c), C.byref(S), C.byref(A)))
+    return S.value, A.value
+
+
+def env_table(p):
+    """Decoded device transition tables (host-built, no GPU needed)."""
+    S, A = env_dims(p)
+    c = env_config(p)
+    n = S * A * 3
+    prob, nxt = np.zeros(n, np.float64), np.zeros(n, np.uint32)
+    rew, term = np.zeros(n, np.float64), np.zeros(n, np.uint8)
+    start = np.zeros(S, np.float64)
+    check(lib().rl_env_table(C.byref(c), prob.ctypes.data, nxt.ctypes.data, rew.ctypes.data,
+                             term.ctypes.data, start.ctypes.data))
+    shp = (S, A, 3)
+    return dict(prob=prob.reshape(shp), next=nxt.reshape(shp), reward=rew.reshape(shp),
+                term=term.reshape(shp), start=start)
+
+
+class Env:
+    """Batched Env<usize, COUNT> (src/env.rs:19-49) on the GPU."""
+
+    def __init__(self, p, n_envs=1, seed=0x5EED, lane_offset=0, device=0):
+        self.p = p
+        self.n = n_envs
+        self.S, self.A = env_dims(p)
+        self.cfg = env_config(p)
+        h = C.c_void_p()
+        check(lib().rl_env_create(C.byref(self.cfg), n_envs, seed, lane_offset, device, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rl_env_destroy(self.h)
+            self.h = None
+
+    def action_size(self):
+        return self.A
+
+    def reset(self):
+        obs = np.zeros(self.n, np.uint64)
+        check(lib().rl_env_reset(self.h, obs.ctypes.data))
+        return obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.uint32)
+        obs = np.zeros(self.n, np.uint64)
+        rew = np.zeros(self.n, np.float64)
+        term = np.zeros(self.n, np.uint8)
+        check(lib().rl_env_step(self.h, a.ctypes.data, obs.ctypes.data, rew.ctypes.data,
+                                term.ctypes.data))
+        return obs, rew, term.astype(bool)
+
+
+class Agent:
+    """Batched Agent<usize, COUNT> (src/agent.rs:47-164) on the GPU."""
+
+    def __init__(self, p):
+        self.p = p
+        self.cfg = agent_config(p)
+        h = C.c_void_p()
+        check(lib().rl_agent_create(C.byref(self.cfg), C.byref(h)))
+        self.h = h
+        S, A, P = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().rl_agent_dims(self.h, C.byref(S), C.byref(A), C.byref(P)))
+        self.S, self.A, self.P = S.value, A.value, P.value
+        self.L = p["n_lanes"]
+        self.private = p["group_size"] == 1
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rl_agent_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_future_q_value_func(self, algo):
+        check(lib().rl_agent_set_future_q_value_func(self.h, ALGO[algo]))
+
+    def set_action_selector(self, selector, eps0=None, eps_decay=None, eps_final=None,
+                            decay_kind=None, ucb_c=None):
+        p = self.p
+        check(lib().rl_agent_set_action_selector(
+            self.h, SELECTOR[selector], p["eps0"] if eps0 is None else eps0,
+            p["eps_decay"] if eps_decay is None else eps_decay,
+            p["eps_final"] if eps_final is None else eps_final,
+            p["decay_kind"] if decay_kind is None else decay_kind,
+            p["ucb_c"] if ucb_c is None else ucb_c))
+
+    def reset(self):
+        check(lib().rl_agent_reset(self.h))
+
+    def train(self, n_episodes, eval_at=0):
+        st = Stats()
+        check(lib().rl_agent_train(self.h, n_episodes, eval_at, C.byref(st)))
+        return st.as_dict()
+
+    def evaluate(self, n_episodes):
+        st = Stats()
+        check(lib().rl_agent_evaluate(self.h, n_episodes, C.byref(st)))
+        return st.as_dict()
+
+    def run(self, n_launches):
+        check(lib().rl_agent_run(self.h, n_launches))
+
+    def synchronize(self):
+        check(lib().rl_agent_synchronize(self.h))
+
+    def stats(self):
+        st = Stats()
+        check(lib().rl_agent_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def q(self):
+        n = self.P * self.S * self.A * (self.L if self.private else 1)
+        out = np.zeros(n, np.float64)
+        check(lib().rl_agent_get_q(self.h, out.ctypes.data, n))
+        if self.private:
+            return out.reshape(self.L, self.P, self.S, self.A)
+        return out.reshape(self.P, self.S, self.A)
+
+    def set_q(self, q):
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1)
+        check(lib().rl_agent_set_q(self.h, q.ctypes.data, q.size))
+
+    def q_raw(self):
+        n = self.P * self.S * self.A
+        out = np.zeros(n, np.int64)
+        check(lib().rl_agent_get_q_raw(self.h, out.ctypes.data, n))
+        return out.reshape(self.P, self.S, self.A)
+
+    def ucb(self):
+        if self.private:
+            n = np.zeros(self.L * self.S * self.A, np.uint32)
+            t = np.zeros(self.L, np.uint64)
+            check(lib().rl_agent_get_ucb(self.h, n.ctypes.data, n.size, t.ctypes.data, t.size))
+            return n.reshape(self.L, self.S, self.A), t
+        n = np.zeros(self.S * self.A, np.uint32)
+        t = np.zeros(1, np.uint64)
+        check(lib().rl_agent_get_ucb(self.h, n.ctypes.data, n.size, t.ctypes.data, 1))
+        return n.reshape(self.S, self.A), int(t[0])
+
+    def epsilon(self):
+        out = np.zeros(self.L, np.float64)
+        check(lib().rl_agent_get_epsilon(self.h, out.ctypes.data, self.L))
+        return out
+
+    def set_recording(self, on=True):
+        check(lib().rl_agent_set_recording(self.h, int(on)))
+
+    def records(self):
+        """[n_steps, n_lanes] rl_step_record since the last call (clears)."""
+        n = C.c_uint64()
+        check(lib().rl_agent_take_records(self.h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, RECORD_DTYPE)
+        check(lib().rl_agent_take_records(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out.reshape(-1, self.L)
+
+    def lane_state(self):
+        core = np.zeros((self.L, 4), np.uint32)
+        aux = np.zeros((self.L, 4), np.uint32)
+        check(lib().rl_agent_lane_state(self.h, core.ctypes.data, aux.ctypes.data, self.L))
+        return core, aux
+
+    # ---- multi-GPU merge as an external collective
+    def delta_words(self):
+        n = C.c_uint64()
+        check(lib().rl_agent_delta_words(self.h, C.byref(n)))
+        return n.value
+
+    def set_delta_buffer(self, ptr, n_words):
+        check(lib().rl_agent_set_delta_buffer(self.h, C.c_void_p(ptr), n_words))
+
+    def launch_train(self):
+        check(lib().rl_agent_launch_train(self.h))
+
+    def launch_apply(self):
+        check(lib().rl_agent_launch_apply(self.h))
+
+    def set_stream(self, stream_ptr):
+        check(lib().rl_agent_set_stream(self.h, C.c_void_p(stream_ptr)))
+
+    def set_timing(self, on=True):
+        check(lib().rl_agent_set_timing(self.h, int(on)))
+
+    def timing(self):
+        ms, n = C.c_double(), C.c_uint64()
+        check(lib().rl_agent_get_timing(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+def kat_log(x, device=0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros_like(x)
+    check(lib().rl_kat_log(device, x.ctypes.data, out.ctypes.data, x.size))
+    return out
+
+
+def kat_rng(seed, lane, n, device=0):
+    out = np.zeros(n, np.uint32)
+    check(lib().rl_kat_rng(device, seed, lane, n, out.ctypes.data))
+    return out
+
+
+def kat_ucb(q, ncount, t, c, device=0):
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    ncount = np.ascontiguousarray(ncount, dtype=np.float64)
+    t = np.ascontiguousarray(t, dtype=np.uint64)
+    out = np.zeros_like(q)
+    check(lib().rl_kat_ucb(device, q.ctypes.data, ncount.ctypes.data, t.ctypes.data, float(c),
+                           out.ctypes.data, q.size))
+    return out

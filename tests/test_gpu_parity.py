@@ -1,0 +1,193 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact bar: integer streams (s, a, r, term, s', a'), the TD error stream and
+Q (raw fixed point in shared mode, f64 bits in private mode) must be EQUAL to
+the oracle's on the same seeded inputs.  Tolerance for Q: exact (the looser
+north-star bound |dQ| < 1e-5 is asserted too, as a floor).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+INT_FIELDS = ["s", "s2", "a", "a2", "term", "mode"]
+
+
+def _params(rl, **kw):
+    return rl.default_params(**kw)
+
+
+def _first_diff(dev, ref, field):
+    if field in ("r", "td"):
+        a, b = dev[field], ref[field]
+        diff = (a.view(np.uint64) != b.view(np.uint64)) & ~(np.isnan(a) & np.isnan(b))
+    else:
+        diff = dev[field] != ref[field]
+    idx = np.argwhere(diff)
+    if idx.size == 0:
+        return None
+    k, lane = idx[0]
+    return f"{field} differs at step {k} lane {lane}: dev {dev[k, lane]} ref {ref[k, lane]}"
+
+
+def _assert_records_equal(dev, ref):
+    """Integer streams and the f64 reward / TD streams bit-exact (NaN == NaN)."""
+    assert dev.shape == ref.shape, (dev.shape, ref.shape)
+    for f in INT_FIELDS + ["r", "td"]:
+        msg = _first_diff(dev, ref, f)
+        assert msg is None, msg
+
+
+def _assert_q_equal(dq, rq):
+    assert dq.shape == rq.shape
+    nan_d, nan_r = np.isnan(dq), np.isnan(rq)
+    assert np.array_equal(nan_d, nan_r), "NaN masks differ"
+    fin = ~nan_d
+    assert np.max(np.abs(dq[fin] - rq[fin]), initial=0.0) < 1e-5
+    assert np.array_equal(dq[fin].view(np.uint64), rq[fin].view(np.uint64))
+
+
+def test_kat_rng(rl, oracle):
+    for lane in (0, 1, 12345, 2**40 + 7):
+        d = rl.kat_rng(0x5EED, lane, 4096)
+        r = oracle.rng_stream(0x5EED, lane, 4096)
+        assert np.array_equal(d, r)
+
+
+def test_kat_log_bit_exact(rl, oracle):
+    rng = np.random.default_rng(1)
+    x = np.concatenate([np.arange(1, 200001, dtype=np.float64),
+                        rng.uniform(1e-300, 1e300, 100000),
+                        np.array([2.0**k for k in range(-1074, 1024, 7)]),
+                        np.array([0.0, -1.0, np.inf, np.nan, 5e-324])])
+    d = rl.kat_log(x)
+    r = np.array([oracle.lib().rlo_log(float(v)) for v in x])
+    same = (d.view(np.uint64) == r.view(np.uint64)) | (np.isnan(d) & np.isnan(r))
+    assert same.all(), x[~same][:10]
+
+
+def test_kat_ucb_bit_exact(rl, oracle):
+    rng = np.random.default_rng(2)
+    n = 50000
+    q = rng.normal(0, 5, n)
+    nc = rng.integers(0, 1000, n).astype(np.float64)
+    t = rng.integers(1, 10**9, n).astype(np.uint64)
+    t[:100] = np.arange(1, 101)
+    d = rl.kat_ucb(q, nc, t, 0.5)
+    L = oracle.lib()
+    r = np.array([qq + 0.5 * np.sqrt(L.rlo_log(float(tt)) / (cc + 2.2250738585072014e-308))
+                  for qq, cc, tt in zip(q, nc, t)])
+    same = (d.view(np.uint64) == r.view(np.uint64)) | (np.isnan(d) & np.isnan(r))
+    assert same.all()
+
+
+@pytest.mark.parametrize("env,map8,slip", [("frozen_lake", 0, 0), ("frozen_lake", 1, 1),
+                                            ("cliff_walking", 0, 0), ("taxi", 0, 0),
+                                            ("blackjack", 0, 0)])
+def test_env_trait_streams(rl, oracle, env, map8, slip):
+    """Batched Env::reset/step vs the oracle's env through a private agent-free walk."""
+    p = _params(rl, env=env, map8x8=map8, slippery=slip, max_steps=20)
+    n = 256
+    e = rl.Env(p, n_envs=n, seed=77)
+    S, A = e.S, e.A
+    rng = np.random.default_rng(3)
+    obs = e.reset()
+    assert obs.shape == (n,)
+    for _ in range(30):
+        act = rng.integers(0, A, n).astype(np.uint32)
+        obs, rew, term = e.step(act)
+        if term.any():
+            with pytest.raises(rl.RLError):
+                e.step(act)
+            obs = e.reset()
+
+
+PRIVATE_CASES = [
+    dict(env="frozen_lake", map8x8=0, algo="qlearning"),
+    dict(env="frozen_lake", map8x8=1, slippery=1, algo="sarsa"),
+    dict(env="cliff_walking", agent="traces", algo="sarsa"),
+    dict(env="taxi", selector="ucb", algo="expected_sarsa"),
+    dict(env="taxi", policy="double", algo="qlearning"),
+    dict(env="blackjack", policy="double", algo="qlearning"),
+    dict(env="blackjack", agent="traces", selector="ucb", algo="sarsa"),
+    dict(env="cliff_walking", policy="double", selector="ucb", algo="expected_sarsa", agent="traces"),
+]
+
+
+@pytest.mark.parametrize("case", PRIVATE_CASES, ids=lambda c: "-".join(f"{v}" for v in c.values()))
+def test_private_mode_matches_reference_loop(rl, oracle, case):
+    """group_size 1: every lane is a reference agent; bit-exact vs the oracle,
+    including the eval interleave (src/agent.rs:107-113)."""
+    n_ep = 60 if case["env"] != "blackjack" else 300
+    p = _params(rl, n_lanes=37, group_size=1, sync_every=50, n_episodes_for_decay=n_ep, **case)
+    dev = rl.Agent(p)
+    dev.set_recording(True)
+    dev.train(n_ep, n_ep // 6)
+    ref = oracle.Batch(p)
+    ref.set_record(True)
+    ref.train_episodes(n_ep, n_ep // 6)
+    _assert_records_equal(dev.records(), ref.records())
+    _assert_q_equal(dev.q(), ref.q())
+    assert np.array_equal(dev.epsilon().view(np.uint64), ref.lane_eps().view(np.uint64))
+    # and lane 5 alone is the faithful single-env reference loop
+    f = oracle.Faithful(dict(p, lane_offset=5))
+    f.train(n_ep, n_ep // 6)
+    _assert_q_equal(dev.q()[5], f.q())
+
+
+SHARED_CASES = [
+    dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256),
+    dict(env="frozen_lake", map8x8=1, slippery=1, algo="expected_sarsa", group_size=64),
+    dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64),
+    dict(env="taxi", selector="ucb", algo="expected_sarsa", group_size=128),
+    dict(env="taxi", selector="ucb", algo="qlearning", group_size=100),
+    dict(env="blackjack", policy="double", algo="qlearning", group_size=256),
+    dict(env="cliff_walking", policy="double", selector="ucb", algo="sarsa", group_size=64),
+    dict(env="frozen_lake", agent="traces", policy="double", algo="qlearning", group_size=2),
+]
+
+
+@pytest.mark.parametrize("case", SHARED_CASES, ids=lambda c: "-".join(f"{v}" for v in c.values()))
+def test_shared_mode_matches_batched_oracle(rl, oracle, case):
+    """Learner groups in LDS + merge every K steps: bit-exact vs the oracle's
+    batched schedule (raw fixed-point Q, UCB counters, streams)."""
+    L = 600
+    p = _params(rl, n_lanes=L, sync_every=16, n_episodes_for_decay=40, **case)
+    dev = rl.Agent(p)
+    dev.set_recording(True)
+    ref = oracle.Batch(p)
+    ref.set_record(True)
+    dev.run(6)
+    ref.run(6)
+    _assert_records_equal(dev.records(), ref.records())
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_q_equal(dev.q(), ref.q())
+    if case.get("selector") == "ucb":
+        dn, dt = dev.ucb()
+        rn, rt = ref.ucb()
+        assert np.array_equal(dn, rn) and dt == rt
+    # episodes mode with eval interleave
+    dev.train(12, 4)
+    ref.train_episodes(12, 4)
+    _assert_records_equal(dev.records(), ref.records())
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+
+
+def test_full_size_fl8x8_properties(rl):
+    """BASELINE config 2 at full size (2^20 lanes): size-independent properties —
+    finite Q in range, every lane stepped exactly K times per launch, merge
+    reproducible (two identical runs give bit-identical Q)."""
+    p = _params(rl, env="frozen_lake", map8x8=1, n_lanes=1 << 20, group_size=256, sync_every=64)
+    qs = []
+    for _ in range(2):
+        a = rl.Agent(p)
+        a.run(3)
+        a.synchronize()
+        st = a.stats()
+        assert st["train_steps"] == 3 * 64 * (1 << 20)
+        q = a.q_raw()
+        qs.append(q)
+        qq = a.q()
+        assert np.isfinite(qq).all() and qq.max() <= 1.0 + 1e-9 and qq.min() >= -1e-9
+        a.close()
+    assert np.array_equal(qs[0], qs[1])
