@@ -775,14 +775,24 @@ struct rlo_batch {
     uint64_t stats[8];
 };
 
+/* Fixed-point Q (shared mode).  |Q raw| <= 2^52, so every entry converts to
+ * f64 exactly and (a+b)/2 of two entries is exact too: comparisons on raw
+ * int64 values are then identical to the reference's f64 comparisons.
+ * delta -> raw: NaN/inf become sticky flags; finite values are clamped to
+ * +-2^51 and rounded half-to-even. */
+#define Q_RAW_MAX ((int64_t)1 << 52)
+#define D_RAW_MAX 0x1p51
 static int64_t q_fix(double d, uint8_t *flag) {
     if (d != d) { *flag |= QF_NAN; return 0; }
     if (d == INFINITY) { *flag |= QF_PINF; return 0; }
     if (d == -INFINITY) { *flag |= QF_NINF; return 0; }
     double x = d * 0x1p40;
-    if (x >= 0x1p62) return (int64_t)1 << 62;
-    if (x <= -0x1p62) return -((int64_t)1 << 62);
+    x = fmax(x, -D_RAW_MAX);
+    x = fmin(x, D_RAW_MAX);
     return (int64_t)rint(x);
+}
+static inline int64_t q_clamp(int64_t v) {
+    return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
 }
 static inline double q_val(int64_t raw, uint8_t fl) {
     if (fl) {
@@ -889,7 +899,7 @@ void rlo_batch_destroy(rlo_batch *b) {
 void rlo_batch_reset(rlo_batch *b) {
     size_t nq = (size_t)b->P * b->S * b->A;
     uint8_t fl = 0;
-    int64_t d = q_fix(b->c.q_default, &fl);
+    int64_t d = q_clamp(q_fix(b->c.q_default, &fl));
     for (size_t i = 0; i < nq; ++i) { b->q_base[i] = d; b->f_base[i] = fl; }
     memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
     b->t_base = 1;
@@ -1058,7 +1068,7 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     }
     if (b->priv) return;
     for (size_t k = 0; k < nq; ++k) {
-        b->q_g[k] = wrap_add(b->q_g[k], mean_delta(b->dq[k], b->dc[k]));
+        b->q_g[k] = q_clamp(b->q_g[k] + mean_delta(b->dq[k], b->dc[k]));
         b->f_g[k] |= b->df[k];
     }
 }
@@ -1112,7 +1122,7 @@ static void run_launch(rlo_batch *b) {
         b->acc_t += (int64_t)(b->t_g - b->t_base);
     }
     for (size_t i = 0; i < nq; ++i) {
-        b->q_base[i] = wrap_add(b->q_base[i], mean_delta(b->acc_q[i], b->acc_c[i]));
+        b->q_base[i] = q_clamp(b->q_base[i] + mean_delta(b->acc_q[i], b->acc_c[i]));
         b->f_base[i] |= b->acc_f[i];
     }
     for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + b->acc_n[i]);

@@ -147,14 +147,30 @@ __device__ __forceinline__ double ucb_value(double q, double c, double lnt, doub
 }
 
 // ------------------------------------------------------------------ fixed-point Q
+// Shared-mode Q entries are int64 fixed point, value = raw * 2^-40, clamped to
+// |raw| <= 2^52 (|Q| <= 4096): every entry — and (a+b)/2 of two entries —
+// converts to f64 exactly, so comparisons on raw int64 are identical to the
+// reference's f64 comparisons (argmax / max without conversions).
+constexpr int64_t Q_RAW_MAX = (int64_t)1 << 52;
+
+// finite delta -> raw: d*2^40 clamped to +-2^51 then rounded half-to-even; the
+// 1.5*2^52 magic add performs rint and the f64->int64 conversion at once.
+__device__ __forceinline__ int64_t q_fix_finite(double d) {
+    double x = d * 0x1p40;
+    x = __builtin_fmax(x, -0x1p51);
+    x = __builtin_fmin(x, 0x1p51);
+    const double y = x + 0x1.8p52;
+    return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
+}
+// with sticky non-finite flags (UCB + expected SARSA)
 __device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag) {
     if (d != d) { flag |= QF_NAN; return 0; }
     if (d == __builtin_inf()) { flag |= QF_PINF; return 0; }
     if (d == -__builtin_inf()) { flag |= QF_NINF; return 0; }
-    const double x = d * 0x1p40;
-    if (x >= 0x1p62) return (int64_t)1 << 62;
-    if (x <= -0x1p62) return -((int64_t)1 << 62);
-    return (int64_t)__builtin_rint(x);
+    return q_fix_finite(d);
+}
+__device__ __forceinline__ int64_t q_clamp(int64_t v) {
+    return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
 }
 __device__ __forceinline__ double q_val(int64_t raw) { return (double)raw * 0x1p-40; }
 __device__ __forceinline__ double q_val(int64_t raw, uint32_t fl) {
@@ -163,6 +179,29 @@ __device__ __forceinline__ double q_val(int64_t raw, uint32_t fl) {
         return (fl & QF_PINF) ? __builtin_inf() : -__builtin_inf();
     }
     return (double)raw * 0x1p-40;
+}
+template <int A>
+__device__ __forceinline__ uint32_t argmax_i64(const int64_t (&v)[A]) {
+    int64_t m = v[0];
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 1; i < A; ++i)
+        if (v[i] > m) { m = v[i]; r = (uint32_t)i; }
+    return r;
+}
+template <int A>
+__device__ __forceinline__ int64_t max_i64(const int64_t (&v)[A]) {
+    int64_t m = v[0];
+#pragma unroll
+    for (int i = 1; i < A; ++i) m = v[i] > m ? v[i] : m;
+    return m;
+}
+template <int A, class T>
+__device__ __forceinline__ T pick(const T (&v)[A], uint32_t i) {   // v[i] as a select chain
+    T r = v[0];
+#pragma unroll
+    for (int j = 1; j < A; ++j) r = (i == (uint32_t)j) ? v[j] : r;
+    return r;
 }
 
 // ------------------------------------------------------------------ utils
@@ -340,21 +379,16 @@ __device__ __forceinline__ void eps_probs(double eps, const double (&q)[A], doub
         if ((uint32_t)i == am) p[i] = 1.0 - eps;
 }
 // sarsa / qlearning / expected_sarsa (src/agent.rs:19-45)
-template <int A>
-__device__ __forceinline__ double future_q(int algo, const double (&q2)[A], uint32_t a2,
-                                           const double (&p)[A]) {
-    if (algo == RL_ALGO_SARSA) {
-        double v = q2[0];
+template <int ALGO, int A>
+__device__ __forceinline__ double future_q(const double (&q2)[A], uint32_t a2, const double (&p)[A]) {
+    if constexpr (ALGO == RL_ALGO_SARSA) return pick<A>(q2, a2);
+    else if constexpr (ALGO == RL_ALGO_QLEARNING) return vmax<A>(q2);
+    else {
+        double f = 0.0;
 #pragma unroll
-        for (int i = 1; i < A; ++i)
-            if ((uint32_t)i == a2) v = q2[i];
-        return v;
+        for (int i = 0; i < A; ++i) f += p[i] * q2[i];
+        return f;
     }
-    if (algo == RL_ALGO_QLEARNING) return vmax<A>(q2);
-    double f = 0.0;
-#pragma unroll
-    for (int i = 0; i < A; ++i) f += p[i] * q2[i];
-    return f;
 }
 // decay_epsilon (uniform_epsilon_greed.rs:42-49) with the bins' closure
 __device__ __forceinline__ double decay_eps(const KParams &p, double eps) {

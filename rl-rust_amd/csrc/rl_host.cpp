@@ -183,13 +183,14 @@ double q_value(int64_t raw, uint32_t fl) {
     }
     return (double)raw * 0x1p-40;
 }
+// host twin of rlamd::q_fix + q_clamp (set_q / q_default): clamp +-2^51, rint
 int64_t q_fix(double d, uint32_t &flag) {
     if (d != d) { flag |= QF_NAN; return 0; }
     if (d == INFINITY) { flag |= QF_PINF; return 0; }
     if (d == -INFINITY) { flag |= QF_NINF; return 0; }
-    const double x = d * 0x1p40;
-    if (x >= 0x1p62) return (int64_t)1 << 62;
-    if (x <= -0x1p62) return -((int64_t)1 << 62);
+    double x = d * 0x1p40;
+    x = std::fmax(x, -0x1p51);
+    x = std::fmin(x, 0x1p51);
     return (int64_t)std::rint(x);
 }
 
@@ -270,7 +271,8 @@ struct rl_agent {
 namespace {
 
 int agent_select_kernel(rl_agent *a) {
-    a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->priv ? 1 : 0);
+    a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo,
+                         a->priv ? 1 : 0);
     if (!a->fn) return fail(RL_E_ARG, "no kernel for this (env, agent, policy, selector)");
     if (a->priv) {
         a->block = dim3(256);
@@ -676,7 +678,7 @@ int rl_agent_set_future_q_value_func(rl_agent *a, int32_t algo) {
     if (!a || algo < 0 || algo > 2) return fail(RL_E_ARG, "bad algo");
     a->cfg.algo = algo;
     agent_sync_params(a);
-    return RL_OK;
+    return agent_select_kernel(a);
 }
 
 int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double eps_decay, double eps_final,

@@ -53,7 +53,7 @@ struct KParams {
     double trunc_reward;
     // hyper-parameters
     double lr, gamma, gl, eps_decay, eps_final, ucb_c;
-    int32_t decay_kind, algo;
+    int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
     // train()/evaluate() control
     uint64_t target_episodes, eval_at;
     uint32_t eval_episodes;
@@ -67,7 +67,7 @@ struct KParams {
 typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, size_t smem,
                                       hipStream_t stream);
 
-train_launch_fn lookup_train(int env, int agent, int policy, int sel, int priv);
+train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
 
 // env-only kernels (batched Env trait) and KAT probes

@@ -5,17 +5,17 @@
 
 namespace rlamd {
 
-train_launch_fn train_table_frozen_lake(int, int, int, int);
-train_launch_fn train_table_cliff_walking(int, int, int, int);
-train_launch_fn train_table_taxi(int, int, int, int);
-train_launch_fn train_table_blackjack(int, int, int, int);
+train_launch_fn train_table_frozen_lake(int, int, int, int, int);
+train_launch_fn train_table_cliff_walking(int, int, int, int, int);
+train_launch_fn train_table_taxi(int, int, int, int, int);
+train_launch_fn train_table_blackjack(int, int, int, int, int);
 
-train_launch_fn lookup_train(int env, int agent, int policy, int sel, int priv) {
+train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv) {
     switch (env) {
-    case RL_ENV_FROZEN_LAKE: return train_table_frozen_lake(agent, policy, sel, priv);
-    case RL_ENV_CLIFF_WALKING: return train_table_cliff_walking(agent, policy, sel, priv);
-    case RL_ENV_TAXI: return train_table_taxi(agent, policy, sel, priv);
-    case RL_ENV_BLACKJACK: return train_table_blackjack(agent, policy, sel, priv);
+    case RL_ENV_FROZEN_LAKE: return train_table_frozen_lake(agent, policy, sel, algo, priv);
+    case RL_ENV_CLIFF_WALKING: return train_table_cliff_walking(agent, policy, sel, algo, priv);
+    case RL_ENV_TAXI: return train_table_taxi(agent, policy, sel, algo, priv);
+    case RL_ENV_BLACKJACK: return train_table_blackjack(agent, policy, sel, algo, priv);
     }
     return nullptr;
 }
@@ -88,7 +88,7 @@ __global__ void k_apply(KParams p, int specials) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int64_t *d = p.delta;
     if (i < PSA) {   // Q_base += mean over the groups (and ranks) that changed the entry
-        p.q_base[i] = (int64_t)((uint64_t)p.q_base[i] + (uint64_t)mean_delta(d[i], d[PSA + i]));
+        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(d[i], d[PSA + i]));
         d[i] = 0;
         d[PSA + i] = 0;
         if (specials) {

@@ -1,9 +1,9 @@
 // rl_train_blackjack.hip — kernel instantiations for RL_ENV_BLACKJACK (one translation unit per env
-// so the 16 specialisations of each env compile in parallel).
+// so the 48 specialisations of each env compile in parallel).
 #include "rl_train_impl.h"
 
 namespace rlamd {
-train_launch_fn train_table_blackjack(int agent, int policy, int sel, int priv) {
-    return train_table_entry<RL_ENV_BLACKJACK>(agent, policy, sel, priv);
+train_launch_fn train_table_blackjack(int agent, int policy, int sel, int algo, int priv) {
+    return train_table_entry<RL_ENV_BLACKJACK>(agent, policy, sel, algo, priv);
 }
 }  // namespace rlamd

@@ -159,16 +159,16 @@ __device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint6
 }
 
 // ======================================================================== shared
-template <int ENV, int AGENT, int POLICY, int SEL>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
     constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
     constexpr bool UCB = SEL == RL_SEL_UCB;
-    const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
-    const bool spec = UCB && p.algo == RL_ALGO_EXPECTED_SARSA;   // inf/NaN possible
-
     constexpr bool TRACES = AGENT == RL_AGENT_TRACES;
+    constexpr bool SPEC = UCB && ALGO == RL_ALGO_EXPECTED_SARSA;  // inf/NaN possible
+    const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
+
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES, S, A, p.n_start, 1);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
@@ -208,50 +208,56 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     LaneRegs L;
     lane_load(p, lane, active, L);
 
-    auto qv = [&](uint32_t idx) -> double {
-        const int64_t raw = (int64_t)Q[idx];
-        if constexpr (UCB) { if (spec) return q_val(raw, QF8[idx]); }
-        return q_val(raw);
+    // f64 image of entry idx (exact: |raw| <= 2^52)
+    auto val = [&](uint32_t idx, int64_t raw) -> double {
+        if constexpr (SPEC) return q_val(raw, QF8[idx]);
+        else return q_val(raw);
     };
-    // add one contribution set (sum of n deltas) to entry idx; returns true for
-    // the first contributor of the step (the entry's owner for the apply phase)
+    // raw rows of state s: table 0 and (double policy) table 1, read once per use
+    auto load_rows = [&](uint32_t s, int64_t (&ra)[A], int64_t (&rb)[A]) {
+#pragma unroll
+        for (int i = 0; i < A; ++i) {
+            ra[i] = (int64_t)Q[s * A + i];
+            rb[i] = P == 2 ? (int64_t)Q[SA + s * A + i] : 0;
+        }
+    };
+    // Agent::get_action = selector(Policy::predict(s)) against the step snapshot;
+    // UCB counter increments are applied by the caller after a barrier.
+    auto select = [&](uint32_t s, const int64_t (&ra)[A], const int64_t (&rb)[A]) -> uint32_t {
+        if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
+            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
+            int64_t v[A];                           // argmax of predict() on exact raw sums
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = P == 2 ? ra[i] + rb[i] : ra[i];
+            return argmax_i64<A>(v);
+        } else {                                    // upper_confidence_bound.rs:29-42
+            double u[A];
+            const double lnt = rl_log((double)T[0]);
+#pragma unroll
+            for (int i = 0; i < A; ++i) {
+                double v = val(s * A + i, ra[i]);
+                if constexpr (P == 2) v = (v + val(SA + s * A + i, rb[i])) / 2.0;
+                u[i] = ucb_value(v, p.ucb_c, lnt, (double)N[s * A + i]);
+            }
+            return argmax<A>(u);
+        }
+    };
+    // add n contributions summing to `sum` to entry idx; true for the step's first
+    // contributor, which owns the entry in the settle phase
     auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
         const uint32_t sh = (idx & 1u) * 16u;
         const uint32_t old = atomicAdd(&CNT[idx >> 1], n << sh);
         if (sum) atomicAdd(&SUM[idx], (unsigned long long)sum);
-        if constexpr (UCB) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
+        if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
         return ((old >> sh) & 0xffffu) == 0u;
     };
-    // owner: Q[idx] += mean of the step's contributions, then clear the accumulators
+    // owner: Q[idx] += mean of the step's contributions (clamped), clear accumulators
     auto settle = [&](uint32_t idx) {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
-        Q[idx] = Q[idx] + (unsigned long long)mean_delta(sum, (int64_t)n);
+        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta(sum, (int64_t)n));
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
-    };
-    // Policy::predict (tabular_policy.rs:27-29; double_tabular_policy.rs:31-40)
-    auto predict = [&](uint32_t s, double (&v)[A]) {
-#pragma unroll
-        for (int i = 0; i < A; ++i) {
-            if constexpr (P == 1) v[i] = qv(s * A + i);
-            else v[i] = (qv(s * A + i) + qv(SA + s * A + i)) / 2.0;
-        }
-    };
-    // Agent::get_action against the snapshot (UCB increments applied by the caller)
-    auto select = [&](uint32_t s) -> uint32_t {
-        double v[A];
-        predict(s, v);
-        if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
-            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
-            return argmax<A>(v);
-        } else {                                    // upper_confidence_bound.rs:29-42
-            const double lnt = rl_log((double)T[0]);
-            double u[A];
-#pragma unroll
-            for (int i = 0; i < A; ++i) u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)N[s * A + i]);
-            return argmax<A>(u);
-        }
     };
 
     for (uint32_t k = 0; k < p.K; ++k) {
@@ -260,7 +266,9 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         if (doR) {
             L.s = E::reset(L.z, L.rng, tabs);
             L.ready = true;
-            L.a = select(L.s);
+            int64_t ra[A], rb[A];
+            load_rows(L.s, ra, rb);
+            L.a = select(L.s, ra, rb);
             L.need_reset = false;
             L.epi_reward = 0.0;
             L.epi_len = 0;
@@ -279,11 +287,15 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         uint32_t s2 = 0, a2 = 0;
         double r = 0.0;
         bool term = false;
+        int64_t ra2[A], rb2[A];
+#pragma unroll
+        for (int i = 0; i < A; ++i) { ra2[i] = 0; rb2[i] = 0; }
         if (alive) {
             uint32_t pos = L.s;
             E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
-            a2 = select(s2);
+            load_rows(s2, ra2, rb2);
+            a2 = select(s2, ra2, rb2);
         }
         if constexpr (UCB) {
             __syncthreads();
@@ -293,17 +305,24 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             __syncthreads();
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
+        // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
         const bool train = alive && L.mode == RL_MODE_TRAIN;
         const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;   // get_values: flag ? alpha : beta
         const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;    // update:     flag ? beta : alpha
         double td = 0.0;
-        int64_t dq = 0;
-        uint32_t dfl = 0;
         if (train) {
-            double q2[A], pr[A];
+            int64_t rv[A];
 #pragma unroll
-            for (int i = 0; i < A; ++i) { q2[i] = qv(vt * SA + s2 * A + i); pr[i] = 0.0; }
-            if (p.algo == RL_ALGO_EXPECTED_SARSA) {
+            for (int i = 0; i < A; ++i) rv[i] = vt ? rb2[i] : ra2[i];
+            double fq;
+            if constexpr (ALGO == RL_ALGO_QLEARNING && !SPEC) {
+                fq = q_val(max_i64<A>(rv));                // utils::max on exact images
+            } else if constexpr (ALGO == RL_ALGO_SARSA && !SPEC) {
+                fq = q_val(pick<A>(rv, a2));
+            } else {
+                double q2[A], pr[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) q2[i] = val(vt * SA + s2 * A + i, rv[i]);
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
@@ -317,23 +336,28 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 #pragma unroll
                     for (int i = 0; i < A; ++i) pr[i] /= sum;
                 }
+                fq = future_q<ALGO, A>(q2, a2, pr);
             }
-            const double fq = future_q<A>(p.algo, q2, a2, pr);
-            const double qa = qv(vt * SA + L.s * A + L.a);
+            const uint32_t qidx = vt * SA + L.s * A + L.a;
+            const double qa = val(qidx, (int64_t)Q[qidx]);
             td = r + p.gamma * fq - qa;
-            if constexpr (AGENT == RL_AGENT_ONE_STEP) dq = q_fix(p.lr * td, dfl);
         }
-        __syncthreads();   // every Q read of this step happened before any write
-        if constexpr (AGENT == RL_AGENT_ONE_STEP) {
+        if constexpr (!TRACES) {
             const uint32_t idx = ut * SA + L.s * A + L.a;
             bool owner = false;
-            if (train) owner = contribute(idx, dq, 1u, dfl);
-            __syncthreads();   // all contributions in
+            if (train) {
+                uint32_t fl = 0;
+                int64_t dq;
+                if constexpr (SPEC) dq = q_fix(p.lr * td, fl);
+                else dq = q_fix_finite(p.lr * td);
+                owner = contribute(idx, dq, 1u, fl);
+            }
+            __syncthreads();   // all contributions in, all Q reads done
             if (owner) settle(idx);
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda.  Per-lane deltas
-            // are summed exactly across the wave, one ds_add_u64 per entry.
+            // are summed exactly across the wave; one contribution per wave and entry.
             const uint64_t Ls = p.L;
             if (train) {
                 double *e = &p.trace[(uint64_t)(L.s * A + L.a) * Ls + lane];
@@ -355,7 +379,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                         if (has) {
                             double *ep = &p.trace[(uint64_t)(o * A + b) * Ls + lane];
                             const double ev = *ep;
-                            d = q_fix(p.lr * (td * ev), fl);
+                            if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
+                            else d = q_fix_finite(p.lr * (td * ev));
                             *ep = ev * p.gl;
                         }
 #pragma unroll
@@ -364,7 +389,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                             const int64_t sum = wave_sum_i64(mine_t ? d : 0);
                             const uint32_t n = (uint32_t)__popcll(__ballot(mine_t));
                             uint32_t f = 0;
-                            if constexpr (UCB) f = wave_or_u32(mine_t ? fl : 0u);
+                            if constexpr (SPEC) f = wave_or_u32(mine_t ? fl : 0u);
                             const uint32_t idx = (uint32_t)t * SA + o * A + b;
                             if ((tid & 63u) == 0 && n) {
                                 if (contribute(idx, sum, n, f)) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
@@ -385,7 +410,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                     p.visited[(uint64_t)w * Ls + lane] = 0u;
                 }
             }
-            __syncthreads();   // all contributions in
+            __syncthreads();   // all contributions in, all Q reads done
             const uint32_t n_touched = LISTN[0];
             for (uint32_t i = tid; i < n_touched; i += nthr) settle(LIST[i]);
             __syncthreads();
@@ -395,7 +420,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         if (alive) {
             if (train) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
-                if (term) { if constexpr (!UCB) L.eps = decay_eps(p, L.eps); }
+                if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
                 L.n_train++;
             } else {
                 L.n_eval++;
@@ -411,8 +436,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     flush_stats(p, L, active);
 
     // ---------------- emit this group's ΔQ (and ΔN, Δt, new flags) for the merge
-    __syncthreads();
     // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts]
+    __syncthreads();
     for (uint32_t i = tid; i < PSA; i += nthr) {
         const int64_t d = (int64_t)(Q[i] - (unsigned long long)p.q_base[i]);
         if (d) {
@@ -429,7 +454,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             const int64_t d = (int64_t)(T[0] - p.t_base[0]);
             if (d) atomicAdd((unsigned long long *)&p.delta[2 * PSA + SA], (unsigned long long)d);
         }
-        if (spec) {
+        if constexpr (SPEC) {
             int64_t *fc = p.delta + 2 * PSA + SA + 1;
             for (uint32_t i = tid; i < PSA; i += nthr) {
                 const uint32_t nf = QF8[i] & ~p.qf_base[i];
@@ -442,7 +467,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 }
 
 // ======================================================================== private
-template <int ENV, int AGENT, int POLICY, int SEL>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -466,8 +491,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
 
     const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
-    const bool active = lane < p.L;
-    if (!active) return;
+    if (lane >= p.L) return;                 // no barrier after this point
     LaneRegs L;
     lane_load(p, lane, true, L);
     const uint64_t Ls = p.L;
@@ -531,7 +555,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
             double q2[A], pr[A];
 #pragma unroll
             for (int i = 0; i < A; ++i) { q2[i] = qref(vt * SA + s2 * A + i); pr[i] = 0.0; }
-            if (p.algo == RL_ALGO_EXPECTED_SARSA) {
+            if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) {
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {
@@ -547,7 +571,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
                     for (int i = 0; i < A; ++i) pr[i] /= sum;
                 }
             }
-            const double fq = future_q<A>(p.algo, q2, a2, pr);
+            const double fq = future_q<ALGO, A>(q2, a2, pr);
             const double qa = qref(vt * SA + L.s * A + L.a);
             td = r + p.gamma * fq - qa;
             if constexpr (AGENT == RL_AGENT_ONE_STEP) {
@@ -586,7 +610,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
                 }
             }
             if (P == 2) L.dflag = !L.dflag;
-            if (term) { if constexpr (!UCB) L.eps = decay_eps(p, L.eps); }
+            if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
             L.n_train++;
         } else {
             L.n_eval++;
@@ -605,26 +629,30 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
 }
 
 // ---------------------------------------------------------------- launch table
-template <int ENV, int AGENT, int POLICY, int SEL, int PRIV>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int PRIV>
 hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream) {
-    const void *k = PRIV ? (const void *)k_train_private<ENV, AGENT, POLICY, SEL>
-                         : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL>;
+    const void *k = PRIV ? (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>
+                         : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO>;
     if (smem > 64 * 1024) {   // gfx950: a workgroup may use up to the CU's 160 KiB of LDS
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
     if constexpr (PRIV)
-        hipLaunchKernelGGL((k_train_private<ENV, AGENT, POLICY, SEL>), grid, block, smem, stream, p);
+        hipLaunchKernelGGL((k_train_private<ENV, AGENT, POLICY, SEL, ALGO>), grid, block, smem, stream, p);
     else
-        hipLaunchKernelGGL((k_train_shared<ENV, AGENT, POLICY, SEL>), grid, block, smem, stream, p);
+        hipLaunchKernelGGL((k_train_shared<ENV, AGENT, POLICY, SEL, ALGO>), grid, block, smem, stream, p);
     return hipGetLastError();
 }
 
 template <int ENV>
-train_launch_fn train_table_entry(int agent, int policy, int sel, int priv) {
-#define RLAMD_E(AG, PO, SE, PR)                                                                    \
-    if (agent == AG && policy == PO && sel == SE && priv == PR) return &launch_train<ENV, AG, PO, SE, PR>;
-#define RLAMD_E2(AG, PO, SE) RLAMD_E(AG, PO, SE, 0) RLAMD_E(AG, PO, SE, 1)
+train_launch_fn train_table_entry(int agent, int policy, int sel, int algo, int priv) {
+#define RLAMD_E(AG, PO, SE, AL, PR)                                                                \
+    if (agent == AG && policy == PO && sel == SE && algo == AL && priv == PR)                      \
+        return &launch_train<ENV, AG, PO, SE, AL, PR>;
+#define RLAMD_E1(AG, PO, SE, AL) RLAMD_E(AG, PO, SE, AL, 0) RLAMD_E(AG, PO, SE, AL, 1)
+#define RLAMD_E2(AG, PO, SE)                                                                       \
+    RLAMD_E1(AG, PO, SE, RL_ALGO_SARSA) RLAMD_E1(AG, PO, SE, RL_ALGO_QLEARNING)                     \
+    RLAMD_E1(AG, PO, SE, RL_ALGO_EXPECTED_SARSA)
 #define RLAMD_E3(AG, PO) RLAMD_E2(AG, PO, RL_SEL_EPS_GREEDY) RLAMD_E2(AG, PO, RL_SEL_UCB)
 #define RLAMD_E4(AG) RLAMD_E3(AG, RL_POLICY_TABULAR) RLAMD_E3(AG, RL_POLICY_DOUBLE)
     RLAMD_E4(RL_AGENT_ONE_STEP)
@@ -632,6 +660,7 @@ train_launch_fn train_table_entry(int agent, int policy, int sel, int priv) {
 #undef RLAMD_E4
 #undef RLAMD_E3
 #undef RLAMD_E2
+#undef RLAMD_E1
 #undef RLAMD_E
     return nullptr;
 }
