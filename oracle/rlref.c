@@ -470,6 +470,24 @@ static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint3
     return 0;
 }
 
+int rlo_env_walk(const rlo_config *c, uint64_t lane, uint32_t n, const uint32_t *actions, uint32_t *s0,
+                 uint32_t *s_next, double *reward, uint8_t *term) {
+    static envdef E;
+    if (build_env(&E, c)) return -1;
+    envstate st;
+    rlo_rng r;
+    memset(&st, 0, sizeof st);
+    rng_seed(&r, c->seed, lane);
+    if (c->env == RLO_ENV_BLACKJACK) bj_initialize_hands(&st, &r);
+    *s0 = env_reset(&E, &st, &r);
+    for (uint32_t i = 0; i < n; ++i) {
+        int tm = 0;
+        if (env_step(&E, &st, actions[i], &r, &s_next[i], &reward[i], &tm)) return (int)i;
+        term[i] = (uint8_t)tm;
+    }
+    return (int)n;
+}
+
 /* ======================================================================== */
 /* action selection & TD targets (shared by both restatements)              */
 /* ======================================================================== */
@@ -1073,15 +1091,22 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     }
 }
 
-static void run_launch(rlo_batch *b) {
+/* Merge delta, same layout as the GPU's (rl_kparams.h):
+ * [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts] (int64).  It is
+ * a plain integer sum over groups, so shards (GPUs) can add theirs with an
+ * all-reduce and every rank applies the identical total. */
+uint64_t rlo_batch_delta_words(const rlo_batch *b) {
+    const size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
+    return 2 * nq + nsa + 1 + 3 * nq;
+}
+
+/* run every local group for K synchronous steps and ADD its changes to delta
+ * (shared mode); private mode just runs the lanes (delta untouched) */
+void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
     size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
-    memset(b->acc_q, 0, nq * 8); memset(b->acc_c, 0, nq * 8); memset(b->acc_f, 0, nq);
-    memset(b->acc_n, 0, nsa * 8);
-    b->acc_t = 0;
     rlo_record *tmp = b->record ? (rlo_record *)malloc(sizeof(rlo_record) * b->G) : NULL;
     size_t rec0 = b->records.n;
     if (b->record) {
-        /* reserve [K][n_lanes] records */
         rlo_record z;
         memset(&z, 0, sizeof z);
         for (size_t i = 0; i < (size_t)b->K * b->c.n_lanes; ++i) vpush(&b->records, &z);
@@ -1097,10 +1122,10 @@ static void run_launch(rlo_batch *b) {
             L->t = b->t_g;
         }
         b->n_g = b->n_g_own;
-        b->stats[6]++;
         free(tmp);
         return;
     }
+    int64_t *dsum = delta, *dcnt = delta + nq, *dn = delta + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
     for (uint32_t g = 0; g < b->n_groups; ++g) {
         uint32_t lane0 = g * b->G;
         uint32_t nl = b->c.n_lanes - lane0 < b->G ? b->c.n_lanes - lane0 : b->G;
@@ -1115,20 +1140,40 @@ static void run_launch(rlo_batch *b) {
         }
         for (size_t i = 0; i < nq; ++i) {
             const int64_t d = (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]);
-            if (d) { b->acc_q[i] = wrap_add(b->acc_q[i], d); b->acc_c[i] += 1; }
-            b->acc_f[i] |= b->f_g[i];
+            if (d) { dsum[i] = wrap_add(dsum[i], d); dcnt[i] += 1; }
+            const uint8_t nf = (uint8_t)(b->f_g[i] & ~b->f_base[i]);
+            if (nf & QF_NAN) fc[i] += 1;
+            if (nf & QF_PINF) fc[nq + i] += 1;
+            if (nf & QF_NINF) fc[2 * nq + i] += 1;
         }
-        for (size_t i = 0; i < nsa; ++i) b->acc_n[i] += (int64_t)b->n_g[i] - (int64_t)b->n_base[i];
-        b->acc_t += (int64_t)(b->t_g - b->t_base);
+        for (size_t i = 0; i < nsa; ++i) dn[i] += (int64_t)b->n_g[i] - (int64_t)b->n_base[i];
+        *dt += (int64_t)(b->t_g - b->t_base);
     }
-    for (size_t i = 0; i < nq; ++i) {
-        b->q_base[i] = q_clamp(b->q_base[i] + mean_delta(b->acc_q[i], b->acc_c[i]));
-        b->f_base[i] |= b->acc_f[i];
-    }
-    for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + b->acc_n[i]);
-    b->t_base = (uint64_t)((int64_t)b->t_base + b->acc_t);
-    b->stats[6]++;
     free(tmp);
+}
+
+/* Q_base += mean over groups that changed each entry (clamped); counters summed */
+void rlo_batch_apply_delta(rlo_batch *b, const int64_t *delta) {
+    size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
+    const int64_t *dsum = delta, *dcnt = delta + nq, *dn = delta + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
+    if (b->priv) { b->stats[6]++; return; }
+    for (size_t i = 0; i < nq; ++i) {
+        b->q_base[i] = q_clamp(b->q_base[i] + mean_delta(dsum[i], dcnt[i]));
+        if (fc[i]) b->f_base[i] |= QF_NAN;
+        if (fc[nq + i]) b->f_base[i] |= QF_PINF;
+        if (fc[2 * nq + i]) b->f_base[i] |= QF_NINF;
+    }
+    for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + dn[i]);
+    b->t_base = (uint64_t)((int64_t)b->t_base + *dt);
+    b->stats[6]++;
+}
+
+static void run_launch(rlo_batch *b) {
+    const uint64_t nw = rlo_batch_delta_words(b);
+    int64_t *delta = (int64_t *)calloc(nw, 8);
+    rlo_batch_launch_groups(b, delta);
+    rlo_batch_apply_delta(b, delta);
+    free(delta);
 }
 
 void rlo_batch_run(rlo_batch *b, uint32_t n_launches) {

@@ -79,6 +79,11 @@ int      rlo_env_dims(const rlo_config *c, uint32_t *n_states, uint32_t *n_actio
 /* transition table export: for each (s,a) up to 3 outcomes (prob, next, reward, term) */
 int      rlo_env_table(const rlo_config *c, double *prob, uint32_t *next, double *reward, uint8_t *term);
 int      rlo_env_start(const rlo_config *c, double *start);   /* initial-state distribution */
+/* Env::reset then Env::step(actions[i]) for i < n on the stream (seed, lane);
+ * writes s0 then per step (s', r, term); returns steps taken before EnvNotReady
+ * (a step after termination stops the walk), -1 on bad config */
+int      rlo_env_walk(const rlo_config *c, uint64_t lane, uint32_t n, const uint32_t *actions,
+                      uint32_t *s0, uint32_t *s_next, double *reward, uint8_t *term);
 
 /* ---------------- faithful single-env restatement (f64) ---------------- */
 typedef struct rlo_faithful rlo_faithful;
@@ -107,6 +112,11 @@ uint64_t rlo_faithful_bench(const rlo_config *c, uint64_t n_episodes, uint64_t e
 typedef struct rlo_batch rlo_batch;
 rlo_batch *rlo_batch_create(const rlo_config *c);
 void   rlo_batch_destroy(rlo_batch *b);
+/* one launch split for multi-rank use: run local groups, ADD their changes to
+ * `delta` (GPU layout, rlo_batch_delta_words int64), then apply the (all-reduced) total */
+uint64_t rlo_batch_delta_words(const rlo_batch *b);
+void   rlo_batch_launch_groups(rlo_batch *b, int64_t *delta);
+void   rlo_batch_apply_delta(rlo_batch *b, const int64_t *delta);
 /* run `n_launches` launches of K = sync_every synchronous steps each */
 void   rlo_batch_run(rlo_batch *b, uint32_t n_launches);
 /* Agent::train for every lane: launches until every lane has finished n_episodes

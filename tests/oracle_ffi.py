@@ -100,6 +100,8 @@ def lib():
         L.rlo_env_dims.argtypes = [P(Config), P(C.c_uint32), P(C.c_uint32)]
         L.rlo_env_table.argtypes = [P(Config), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rlo_env_start.argtypes = [P(Config), C.c_void_p]
+        L.rlo_env_walk.argtypes = [P(Config), C.c_uint64, C.c_uint32, C.c_void_p, P(C.c_uint32),
+                                   C.c_void_p, C.c_void_p, C.c_void_p]
         L.rlo_faithful_create.restype = C.c_void_p
         L.rlo_faithful_create.argtypes = [P(Config)]
         L.rlo_faithful_destroy.argtypes = [C.c_void_p]
@@ -135,6 +137,10 @@ def lib():
         L.rlo_batch_set_record.argtypes = [C.c_void_p, C.c_int]
         L.rlo_batch_take_records.restype = C.c_uint64
         L.rlo_batch_take_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.rlo_batch_delta_words.restype = C.c_uint64
+        L.rlo_batch_delta_words.argtypes = [C.c_void_p]
+        L.rlo_batch_launch_groups.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_apply_delta.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_n_records.restype = C.c_uint64
         L.rlo_batch_n_records.argtypes = [C.c_void_p]
         L.rlo_batch_stats.argtypes = [C.c_void_p, C.c_void_p]
@@ -168,6 +174,21 @@ def env_table(p):
     shp = (S, A, 3)
     return dict(prob=prob.reshape(shp), next=nxt.reshape(shp), reward=rew.reshape(shp),
                 term=term.reshape(shp), start=start)
+
+
+def env_walk(p, actions, lane=0):
+    """Env::reset + Env::step(a) for each action; stops at EnvNotReady."""
+    c = make_config(p)
+    a = np.ascontiguousarray(actions, dtype=np.uint32)
+    n = a.size
+    s0 = C.c_uint32()
+    s2 = np.zeros(n, np.uint32)
+    r = np.zeros(n, np.float64)
+    t = np.zeros(n, np.uint8)
+    k = lib().rlo_env_walk(C.byref(c), lane, n, a.ctypes.data, C.byref(s0), s2.ctypes.data,
+                           r.ctypes.data, t.ctypes.data)
+    assert k >= 0
+    return s0.value, s2[:k], r[:k], t[:k].astype(bool), k
 
 
 def rng_stream(seed, lane, n):
@@ -306,6 +327,17 @@ class Batch:
         out = np.zeros(n, RECORD_DTYPE)
         lib().rlo_batch_take_records(self.h, out.ctypes.data, n)
         return out.reshape(-1, self.L)
+
+    def delta_words(self):
+        return lib().rlo_batch_delta_words(self.h)
+
+    def launch_groups(self, delta):
+        """run local groups for K steps, adding their merge delta into `delta` (int64)"""
+        assert delta.dtype == np.int64 and delta.flags.c_contiguous
+        lib().rlo_batch_launch_groups(self.h, delta.ctypes.data)
+
+    def apply_delta(self, delta):
+        lib().rlo_batch_apply_delta(self.h, np.ascontiguousarray(delta, np.int64).ctypes.data)
 
     def stats(self):
         out = np.zeros(8, np.uint64)

@@ -85,21 +85,56 @@ def test_kat_ucb_bit_exact(rl, oracle):
                                             ("cliff_walking", 0, 0), ("taxi", 0, 0),
                                             ("blackjack", 0, 0)])
 def test_env_trait_streams(rl, oracle, env, map8, slip):
-    """Batched Env::reset/step vs the oracle's env through a private agent-free walk."""
-    p = _params(rl, env=env, map8x8=map8, slippery=slip, max_steps=20)
-    n = 256
+    """Batched Env::reset/step on the GPU == the oracle's env walked with the
+    same per-lane stream and actions (obs as the reference's usize ids)."""
+    p = _params(rl, env=env, map8x8=map8, slippery=slip, max_steps=12, seed=77)
+    n, T = 64, 16
     e = rl.Env(p, n_envs=n, seed=77)
-    S, A = e.S, e.A
     rng = np.random.default_rng(3)
-    obs = e.reset()
-    assert obs.shape == (n,)
-    for _ in range(30):
-        act = rng.integers(0, A, n).astype(np.uint32)
-        obs, rew, term = e.step(act)
-        if term.any():
-            with pytest.raises(rl.RLError):
-                e.step(act)
-            obs = e.reset()
+    acts = rng.integers(0, e.A, (T, n)).astype(np.uint32)
+    obs0 = e.reset()
+    dev_s, dev_r, dev_t = [], [], []
+    alive = np.ones(n, bool)
+    for k in range(T):
+        if not alive.all():
+            break
+        s2, r, t = e.step(acts[k])
+        dev_s.append(s2); dev_r.append(r); dev_t.append(t)
+        alive &= ~t
+    steps = len(dev_s)
+    if steps < T:
+        with pytest.raises(rl.RLError) as ex:      # some lane terminated: batched EnvNotReady
+            e.step(acts[steps])
+        assert ex.value.code == 1
+    for lane in range(n):
+        s0, s2, r, t, k = oracle.env_walk(p, acts[:steps, lane], lane=lane)
+        ref0 = s0 if env != "blackjack" else oracle.lib().rlo_blackjack_obs_id(
+            s0 // 54, (s0 >> 1) % 27, s0 & 1)
+        assert obs0[lane] == ref0
+        m = min(k, steps)
+        for j in range(m):
+            ref = s2[j] if env != "blackjack" else oracle.lib().rlo_blackjack_obs_id(
+                s2[j] // 54, (s2[j] >> 1) % 27, s2[j] & 1)
+            assert dev_s[j][lane] == ref and dev_r[j][lane] == r[j] and dev_t[j][lane] == t[j]
+
+
+def test_env_trait_known_paths(rl):
+    """Hand-derived KATs (tests/golden/tables.json) on the GPU env kernels."""
+    import json, os
+    kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tables.json")))["kat"]
+    e = rl.Env(_params(rl, env="frozen_lake"), n_envs=1)
+    assert e.reset()[0] == 0
+    for a, s in zip(kat["fl4x4_path"]["actions"], kat["fl4x4_path"]["states"]):
+        s2, r, t = e.step([a])
+        assert s2[0] == s
+    assert r[0] == 1.0 and t[0]
+    e = rl.Env(_params(rl, env="cliff_walking"), n_envs=1)
+    assert e.reset()[0] == 36
+    tot = 0.0
+    for a in kat["cliff_path"]["actions"]:
+        s2, r, t = e.step([a])
+        tot += r[0]
+    assert tot == -13.0 and s2[0] == 47 and t[0]
 
 
 PRIVATE_CASES = [

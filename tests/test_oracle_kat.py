@@ -1,0 +1,142 @@
+"""CPU: pin the oracle against the reference-derived fixtures.
+
+tests/golden/tables.json holds (a) an independent Python restatement of every
+transition table / start distribution and (b) known answers derived by hand
+from the reference source (SURVEY §8c iii).  The reference itself cannot run
+here (Rust, no toolchain), so this is the oracle's pinning.
+"""
+import ctypes
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tables.json")))
+KAT = GOLD["kat"]
+
+ENV_CASES = [("frozen_lake_4x4_det", dict(env="frozen_lake", map8x8=0, slippery=0)),
+             ("frozen_lake_4x4_slippery", dict(env="frozen_lake", map8x8=0, slippery=1)),
+             ("frozen_lake_8x8_det", dict(env="frozen_lake", map8x8=1, slippery=0)),
+             ("frozen_lake_8x8_slippery", dict(env="frozen_lake", map8x8=1, slippery=1)),
+             ("cliff_walking", dict(env="cliff_walking")),
+             ("taxi", dict(env="taxi"))]
+
+
+@pytest.mark.parametrize("name,kw", ENV_CASES, ids=[c[0] for c in ENV_CASES])
+def test_oracle_tables_match_independent_restatement(oracle, name, kw):
+    g = GOLD[name]
+    t = oracle.env_table(oracle.default_params(**kw))
+    for f in ("prob", "next", "reward", "term"):
+        assert np.array_equal(t[f], np.array(g[f], dtype=t[f].dtype)), f
+    assert np.array_equal(t["start"], np.array(g["start"]))
+
+
+def test_fl4x4_known_path(oracle):
+    k = KAT["fl4x4_path"]
+    s0, s2, r, term, n = oracle.env_walk(oracle.default_params(env="frozen_lake"), k["actions"])
+    assert s0 == 0 and n == len(k["actions"])
+    assert list(s2) == k["states"] and r[-1] == k["final_reward"] and term[-1] and not term[:-1].any()
+
+
+def test_cliff_known_paths(oracle):
+    k = KAT["cliff_path"]
+    s0, s2, r, term, n = oracle.env_walk(oracle.default_params(env="cliff_walking"), k["actions"])
+    assert s0 == 36 and r.sum() == k["total_reward"] and s2[-1] == k["final_state"] and term[-1]
+    k = KAT["cliff_fall"]
+    _, s2, r, term, _ = oracle.env_walk(oracle.default_params(env="cliff_walking"), k["actions"])
+    assert s2[0] == k["state"] and r[0] == k["reward"] and term[0]
+
+
+@pytest.mark.parametrize("env,r_trunc", [("frozen_lake", 0.0), ("cliff_walking", -100.0), ("taxi", 0.0)])
+def test_truncation_returns_state_zero(oracle, env, r_trunc):
+    """frozen_lake.rs:119-122 (and cliff/taxi): step max_steps+1 -> (0, r_trunc, true)."""
+    p = oracle.default_params(env=env, max_steps=3)
+    acts = [3, 3, 3, 3] if env != "taxi" else [1, 1, 1, 1]
+    _, s2, r, term, n = oracle.env_walk(p, acts)
+    assert n == 4 and s2[3] == 0 and r[3] == r_trunc and term[3] and not term[:3].any()
+    _, _, _, _, n = oracle.env_walk(p, acts + [0])          # one more step: EnvNotReady
+    assert n == 4
+
+
+def test_frozen_lake_draws_even_when_deterministic(oracle):
+    """frozen_lake.rs:126 draws a uniform every step: walks with the same seed but
+    different lengths consume different stream prefixes identically."""
+    p = oracle.default_params(env="frozen_lake", map8x8=1, slippery=1, seed=5)
+    _, a, _, _, _ = oracle.env_walk(p, [2] * 6)
+    _, b, _, _, _ = oracle.env_walk(p, [2] * 3)
+    assert list(a[:3]) == list(b)
+
+
+def test_kat_constants(oracle):
+    L = oracle.lib()
+    assert KAT["taxi_encode_4_3_4_2"] == 478
+    t = oracle.env_table(oracle.default_params(env="taxi"))
+    assert np.cumsum(t["start"])[-1] != 1.0
+    acc = 0.0
+    for v in t["start"]:
+        acc += v
+    assert acc == KAT["taxi_start_cumsum_last"] == 0.9999999999999961
+    # slippery FrozenLake running sums, last one exactly 1.0
+    assert KAT["fl_slippery_cumsum"][2] == 1.0
+    # rand 0.8 rejection zones: zone = MAX - ints_to_reject; reject when lo > zone
+    rej = ctypes.c_int()
+    assert KAT["uniform_int_reject_6"] == 4 and KAT["uniform_card_reject"] == 6
+    v = (2**64 - 4) // 6                     # v*6 mod 2^64 = 2^64-4 > 2^64-1-4
+    L.rlo_uniform_int_u64(v, 6, ctypes.byref(rej))
+    assert rej.value == 1
+    assert L.rlo_uniform_int_u64(v - 1, 6, ctypes.byref(rej)) == 0 and rej.value == 0
+    assert L.rlo_uniform_int_u64(2**64 - 1, 4, ctypes.byref(rej)) == 3 and rej.value == 0
+    assert L.rlo_uniform_card_u32(0, ctypes.byref(rej)) == 1 and rej.value == 0
+    assert L.rlo_uniform_card_u32(0xFFFFFFFF, ctypes.byref(rej)) == 10 and rej.value == 0
+    L.rlo_uniform_card_u32((2**32 - 6) // 10, ctypes.byref(rej))   # lo = 2^32-6 > zone
+    assert rej.value == 1
+    # UniformFloat(0..1) endpoints
+    assert L.rlo_u64_to_uniform01(0) == 0.0
+    assert L.rlo_u64_to_uniform01(2**64 - 1) == 1.0 - 2.0**-52
+
+
+def test_ucb_bonus_overflows_at_t55(oracle):
+    """upper_confidence_bound.rs:36: ln(t)/(0 + MIN_POSITIVE) is +inf first at t = 55 (F7)."""
+    L = oracle.lib()
+    assert KAT["ucb_first_inf_t"] == 55
+    assert math.isinf(L.rlo_log(55.0) / 2.2250738585072014e-308)
+    assert not math.isinf(L.rlo_log(54.0) / 2.2250738585072014e-308)
+
+
+@pytest.mark.parametrize("n", [1000, 10000, 100000])
+def test_epsilon_stall_residue(oracle, n):
+    """uniform_epsilon_greed.rs:42-49: eps stops at a positive residue."""
+    eps, k = KAT["eps_stall"][str(n)]
+    f = oracle.Faithful(oracle.default_params(env="frozen_lake", n_episodes_for_decay=n))
+    f.train(k + 5)
+    assert f.epsilon() == eps
+
+
+def test_rlo_log_vs_libm(oracle):
+    """The shared ln() (fdlibm algorithm) is within 1 ulp of glibc's log and
+    equal on the vast majority of UCB arguments (t integer)."""
+    L = oracle.lib()
+    t = np.concatenate([np.arange(1, 20001), np.geomspace(2e4, 1e15, 2000).round()])
+    ours = np.array([L.rlo_log(float(v)) for v in t])
+    ref = np.log(t)
+    ulp = np.abs(ours.view(np.int64) - ref.view(np.int64))
+    assert ulp.max() <= 1
+    assert (ulp == 0).mean() > 0.99
+
+
+def test_rng_stream_deterministic_and_lane_distinct(oracle):
+    a = oracle.rng_stream(0x5EED, 0, 1000)
+    assert np.array_equal(a, oracle.rng_stream(0x5EED, 0, 1000))
+    b = oracle.rng_stream(0x5EED, 1, 1000)
+    assert (a != b).mean() > 0.99
+    # xoshiro128** words look uniform: mean of the top bit ~ 0.5
+    w = oracle.rng_stream(7, 3, 100000)
+    assert abs((w >> 31).mean() - 0.5) < 0.01
+
+
+def test_blackjack_obs_ids_injective(oracle):
+    L = oracle.lib()
+    ids = {L.rlo_blackjack_obs_id(p, d, a) for p in range(32) for d in range(27) for a in range(2)}
+    assert len(ids) == 32 * 27 * 2

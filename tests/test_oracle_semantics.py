@@ -1,0 +1,143 @@
+"""CPU: semantics of the batched schedule (the GPU's contract), checked on the oracle.
+
+* private mode (group_size 1) == the faithful single-env reference loop, bit for bit
+* shared mode: single-group runs are launch-length invariant, Q stays in range,
+  the merge is decomposable across ranks (world_size-2 gloo all-reduce == one
+  process holding every lane), NaN stickiness for UCB + expected SARSA.
+"""
+import itertools
+import os
+import socket
+
+import numpy as np
+import pytest
+
+CONFIGS = list(itertools.product(["frozen_lake", "cliff_walking", "taxi", "blackjack"],
+                                 ["one_step", "traces"], ["tabular", "double"],
+                                 ["eps_greedy", "ucb"], ["sarsa", "qlearning", "expected_sarsa"]))
+
+
+def _eq_nan(a, b):
+    return np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(
+        np.nan_to_num(a).view(np.uint64), np.nan_to_num(b).view(np.uint64))
+
+
+@pytest.mark.parametrize("env,agent,policy,sel,algo", CONFIGS[::5],
+                         ids=lambda v: str(v))
+def test_private_batch_equals_faithful(oracle, env, agent, policy, sel, algo):
+    n = 40 if env != "blackjack" else 200
+    p = oracle.default_params(env=env, agent=agent, policy=policy, selector=sel, algo=algo,
+                              map8x8=1, n_episodes_for_decay=n, n_lanes=3, group_size=1,
+                              sync_every=37)
+    b = oracle.Batch(p)
+    b.set_record(True)
+    b.train_episodes(n, n // 4)
+    recs = b.records()
+    q = b.q()
+    for lane in range(3):
+        f = oracle.Faithful(dict(p, lane_offset=lane))
+        f.set_record(True)
+        f.train(n, n // 4)
+        fr = f.records()
+        br = recs[:, lane]
+        br = br[br["mode"] == oracle.MODE_TRAIN]
+        assert len(fr) == len(br)
+        for k in ("s", "s2", "a", "a2", "term", "r"):
+            assert np.array_equal(fr[k], br[k]), k
+        assert _eq_nan(fr["td"], br["td"])
+        assert _eq_nan(f.q(), q[lane])
+
+
+@pytest.mark.parametrize("env,algo", [("frozen_lake", "qlearning"), ("taxi", "sarsa")])
+def test_single_group_is_launch_length_invariant(oracle, env, algo):
+    """With one learner group every merge is the identity, so K only changes how
+    the steps are cut into launches."""
+    outs = []
+    for K in (10, 50):
+        p = oracle.default_params(env=env, algo=algo, map8x8=1, n_lanes=100, group_size=128,
+                                  sync_every=K)
+        b = oracle.Batch(p)
+        b.set_record(True)
+        b.run(100 // K)
+        outs.append((b.q_raw(), b.records()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for k in ("s", "a", "s2", "td"):
+        assert np.array_equal(outs[0][1][k], outs[1][1][k])
+
+
+def test_shared_mode_stays_in_range(oracle):
+    """The mean combination rule keeps Q a convex-ish average of lane targets:
+    FrozenLake Q stays in [0, 1] even with 4096 lanes and 16 groups."""
+    p = oracle.default_params(env="frozen_lake", map8x8=1, n_lanes=4096, group_size=256, sync_every=32)
+    b = oracle.Batch(p)
+    b.run(20)
+    q = b.q()
+    assert q.min() >= 0.0 and q.max() <= 1.0 + 1e-12 and q.max() > 0.0
+
+
+def test_expected_sarsa_ucb_nan_is_sticky(oracle):
+    """UCB + expected SARSA produces NaN Q entries; they never heal."""
+    p = oracle.default_params(env="taxi", selector="ucb", algo="expected_sarsa", n_lanes=64,
+                              group_size=64, sync_every=64)
+    b = oracle.Batch(p)
+    b.run(4)
+    nan1 = np.isnan(b.q())
+    assert nan1.any()
+    b.run(4)
+    assert np.isnan(b.q())[nan1].all()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, p, n_launch, out_q):
+    import torch
+    import torch.distributed as dist
+
+    import oracle_ffi as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    L = p["n_lanes"] // world
+    b = O.Batch(dict(p, n_lanes=L, lane_offset=rank * L))
+    for _ in range(n_launch):
+        d = np.zeros(b.delta_words(), np.int64)
+        b.launch_groups(d)
+        t = torch.from_numpy(d)
+        dist.all_reduce(t)                     # the RCCL all-reduce of bench.py, on gloo
+        b.apply_delta(t.numpy())
+    out_q.put((rank, b.q_raw().tobytes(), b.ucb()[0].tobytes(), b.ucb()[1]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [dict(env="frozen_lake", map8x8=1, algo="qlearning"),
+                                  dict(env="taxi", selector="ucb", algo="sarsa")],
+                         ids=["fl8x8-q", "taxi-ucb-sarsa"])
+def test_two_rank_merge_equals_one_process(oracle, case):
+    """world_size-2 gloo: each rank holds half the lanes (contiguous global lane
+    ids), all-reduces the int64 merge delta, applies it.  Q and UCB counters
+    must be bit-identical to one process holding every lane (GPU-count
+    independence of the N>1 bench path)."""
+    import torch.multiprocessing as mp
+    p = oracle.default_params(n_lanes=512, group_size=64, sync_every=16, **case)
+    n_launch = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, p, n_launch, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict((r, (qb, nb, t)) for r, qb, nb, t in (q.get(timeout=300) for _ in procs))
+    for pr in procs:
+        pr.join(timeout=60)
+    one = oracle.Batch(p)
+    one.run(n_launch)
+    ref_q = one.q_raw().tobytes()
+    ref_n, ref_t = one.ucb()
+    for r in (0, 1):
+        assert res[r][0] == ref_q
+        assert res[r][1] == ref_n.tobytes() and res[r][2] == ref_t
