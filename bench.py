@@ -136,17 +136,23 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms, n_kern = agent.timing()
     st1 = agent.stats()
+    # every Env::step inside train (truncation included) counted on the device;
+    # RESET steps (env.reset + first get_action) are not env steps
     steps_done = st1["train_steps"] - st0["train_steps"]
-    expect = args.steps * args.sync * args.lanes
-    assert steps_done == expect, (steps_done, expect)
+    assert 0 < steps_done <= args.steps * args.sync * args.lanes, steps_done
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-    total_steps = world * expect
+    if world > 1:
+        ts = torch.tensor([steps_done], dtype=torch.int64, device=f"cuda:{local_rank}")
+        dist.all_reduce(ts)
+        total_steps = int(ts.item())
+    else:
+        total_steps = steps_done
     value = total_steps / wall
     avg_kern_s = kern_ms / max(n_kern, 1) / 1e3
-    bytes_per_launch = BYTES_PER_STEP * args.lanes * args.sync
+    bytes_per_launch = BYTES_PER_STEP * steps_done / args.steps      # env-steps per launch x 32 B
     achieved = bytes_per_launch / avg_kern_s
     traffic = None
     if os.path.exists(args.traffic_file):
@@ -165,7 +171,8 @@ def main():
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
                    "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
-                   "env_steps_per_launch": args.lanes * args.sync, "parallelism": f"dp{world}"},
+                   "env_steps_per_launch": steps_done / args.steps,
+                   "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,

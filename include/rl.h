@@ -88,13 +88,17 @@ typedef struct rl_agent_config {
     int32_t device;       /* HIP device ordinal */
 } rl_agent_config;
 
-/* One per lane per synchronous step (recording mode only): the integer stream
- * (s, a, r, terminated, s', a') plus the TD error pushed to training_error
- * (src/agent.rs:98).  For Blackjack s/s2 are dense indices (see rl_blackjack_obs_id). */
+/* One per lane per synchronous step (recording mode only).  A live lane does
+ * one of two things per step (src/agent.rs:83-106 cut at its get_action calls):
+ *   kind 1 RESET: s = Env::reset(), a = get_action(s)              (s, a set)
+ *   kind 2 STEP:  (s2, r, term) = Env::step(a), a2 = get_action(s2), update;
+ *                 td is the value pushed to training_error (src/agent.rs:98)
+ *   kind 0: lane idle (finished its train()/evaluate() call)
+ * For Blackjack s/s2 are dense indices (see rl_obs_to_reference). */
 typedef struct rl_step_record {
     uint32_t s, s2;
     uint8_t a, a2, term, mode;
-    uint32_t pad;
+    uint8_t kind, pad[3];
     double r, td;
 } rl_step_record;
 

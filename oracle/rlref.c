@@ -970,37 +970,42 @@ static int64_t mean_delta(int64_t sum, int64_t n) {
     return (int64_t)trunc((double)sum / (double)n);
 }
 
+/* One synchronous step of a learner group.  Every live lane does exactly one
+ * of (src/agent.rs:83-106 cut at its get_action calls):
+ *   RESET: s = env.reset(); a = get_action(s)                 (:83-84)
+ *   STEP:  (s',r,term) = env.step(a); a' = get_action(s'); update  (:88-101)
+ * All lanes read the step-start snapshot (Q, UCB N/t); UCB increments are
+ * applied after every selection; Q moves by the mean of the step's deltas.
+ * For one lane this is the reference's sequence exactly. */
 static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *rec) {
     const uint32_t A = b->A;
     const int ucb = b->c.selector == RLO_SEL_UCB;
-    uint32_t sel_s[1024], sel_a[1024];
-    uint32_t nsel = 0;
-    /* ---- R-phase ---- */
-    for (uint32_t j = 0; j < nl; ++j) {
-        lane_t *L = &b->lanes[lane0 + j];
-        if (L->mode == RLO_MODE_DONE || !L->need_reset) continue;
-        L->s = env_reset(&b->E, &L->st, &L->rng);
-        L->a = b_select(b, L, L->s);
-        L->need_reset = 0; L->epi_reward = 0.0; L->epi_len = 0;
-        if (ucb) { sel_s[nsel] = L->s; sel_a[nsel] = L->a; nsel++; }
-    }
-    for (uint32_t i = 0; i < nsel; ++i) b->n_g[(size_t)sel_s[i] * A + sel_a[i]] += 1;
-    b->t_g += nsel;
-    nsel = 0;
-    /* ---- S-phase: env step + next action ---- */
-    uint32_t s2v[1024], a2v[1024];
+    uint32_t s2v[1024], a2v[1024], kind[1024];
     double rv[1024];
     int tv[1024];
+    uint32_t nsel = 0;
+    /* ---- env + selection against the snapshot ---- */
     for (uint32_t j = 0; j < nl; ++j) {
         lane_t *L = &b->lanes[lane0 + j];
+        kind[j] = 0;
         if (L->mode == RLO_MODE_DONE) continue;
-        if (env_step(&b->E, &L->st, L->a, &L->rng, &s2v[j], &rv[j], &tv[j])) abort();
+        if (L->need_reset) {
+            kind[j] = 1;
+            s2v[j] = env_reset(&b->E, &L->st, &L->rng);
+            rv[j] = 0.0; tv[j] = 0;
+        } else {
+            kind[j] = 2;
+            if (env_step(&b->E, &L->st, L->a, &L->rng, &s2v[j], &rv[j], &tv[j])) abort();
+        }
         a2v[j] = b_select(b, L, s2v[j]);
-        if (ucb) { sel_s[nsel] = s2v[j]; sel_a[nsel] = a2v[j]; nsel++; }
+        nsel++;
     }
-    for (uint32_t i = 0; i < nsel; ++i) b->n_g[(size_t)sel_s[i] * A + sel_a[i]] += 1;
-    b->t_g += nsel;
-    /* ---- S-phase: TD update against the Q snapshot ---- */
+    if (ucb) {
+        for (uint32_t j = 0; j < nl; ++j)
+            if (kind[j]) b->n_g[(size_t)s2v[j] * A + a2v[j]] += 1;
+        b->t_g += nsel;
+    }
+    /* ---- TD update of the STEP lanes against the Q snapshot ---- */
     size_t nq = (size_t)b->P * b->S * A;
     memset(b->dq, 0, nq * 8);
     memset(b->dc, 0, nq * 4);
@@ -1008,8 +1013,14 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     for (uint32_t j = 0; j < nl; ++j) {
         lane_t *L = &b->lanes[lane0 + j];
         rlo_record *R = rec ? &rec[j] : NULL;
-        if (R) { memset(R, 0, sizeof *R); R->mode = (uint8_t)L->mode; }
-        if (L->mode == RLO_MODE_DONE) continue;
+        if (R) { memset(R, 0, sizeof *R); R->mode = (uint8_t)L->mode; R->kind = (uint8_t)kind[j]; }
+        if (kind[j] == 0) continue;
+        if (kind[j] == 1) {                   /* RESET: new episode, first action */
+            L->s = s2v[j]; L->a = a2v[j];
+            L->need_reset = 0; L->epi_reward = 0.0; L->epi_len = 0;
+            if (R) { R->s = L->s; R->a = (uint8_t)L->a; }
+            continue;
+        }
         uint32_t s = L->s, a = L->a, s2 = s2v[j], a2 = a2v[j];
         double r = rv[j];
         int term = tv[j];

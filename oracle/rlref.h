@@ -60,11 +60,13 @@ typedef struct {
     uint32_t eval_episodes;   /* episodes per in-train evaluate() call (reference: 100) */
 } rlo_config;
 
-/* one per-lane-per-step record (same layout as the product's rl_step_record) */
+/* one per-lane-per-step record (same layout as the product's rl_step_record).
+ * kind: 0 idle (lane done), 1 RESET (s, a = new episode's state and first
+ * action), 2 STEP (s, a, r, term, s2, a2, td) */
 typedef struct {
     uint32_t s, s2;
     uint8_t a, a2, term, mode;
-    uint32_t pad;
+    uint8_t kind, pad[3];
     double r, td;
 } rlo_record;
 

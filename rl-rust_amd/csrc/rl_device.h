@@ -242,7 +242,13 @@ struct EnvTables {
     const double *cdf;
     uint32_t n_start, max_steps;
     double th1, th2, th3, trunc_reward;
+    int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
 };
+// Env::reset's categorical draw (frozen_lake.rs:107-108, taxi.rs:136-137): the
+// uniform is always consumed; the search is skipped when the answer is fixed.
+__device__ __forceinline__ uint32_t start_state(const EnvTables &t, double u) {
+    return t.fixed_start >= 0 ? (uint32_t)t.fixed_start : cdf_search(t.cdf, t.n_start, u);
+}
 
 template <int ENV> struct EnvDev;
 
@@ -253,7 +259,7 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
     __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
         const double u = uniform01(r);                 // frozen_lake.rs:107-108
         z = 0;
-        return cdf_search(t.cdf, t.n_start, u);
+        return start_state(t, u);
     }
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
@@ -300,7 +306,7 @@ template <> struct EnvDev<RL_ENV_TAXI> {
     __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
         const double u = uniform01(r);                 // taxi.rs:136-137
         z = 0;
-        return cdf_search(t.cdf, t.n_start, u);
+        return start_state(t, u);
     }
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
                                                 const EnvTables &t, uint32_t &s2, double &rew,

@@ -44,6 +44,7 @@ struct EnvHost {
     std::vector<double> start;    // initial-state distribution
     std::vector<double> cdf;      // running sum of `start` (categorical_sample, utils.rs:33-43)
     double th1 = 0, th2 = 0, th3 = 0, trunc_reward = 0;
+    int32_t fixed_start = -1;     // categorical_sample over `cdf` is constant (single start state)
 };
 
 const char *const kFL4[] = {"SFFF", "FHFH", "FFFH", "HFFG"};                     // frozen_lake.rs:23
@@ -72,6 +73,14 @@ void finish_cdf(EnvHost &e) {
     for (size_t i = 0; i < e.start.size(); ++i) {
         b += e.start[i];
         e.cdf[i] = b;
+    }
+    // first i with cdf[i] > u for every u in [0, 1 - 2^-52]: fixed when all
+    // earlier sums are 0 and cdf[i] exceeds the largest uniform
+    e.fixed_start = -1;
+    for (size_t i = 0; i < e.cdf.size(); ++i) {
+        if (e.cdf[i] == 0.0) continue;
+        if (e.cdf[i] > 1.0 - 0x1p-52) e.fixed_start = (int32_t)i;
+        break;
     }
 }
 
@@ -523,6 +532,7 @@ int rl_env_create(const rl_env_config *cfg, uint32_t n, uint64_t seed, uint64_t 
     p.L = n; p.S = e->eh.S; p.A = e->eh.A; p.P = 1;
     p.core = e->core; p.rng = e->rng;
     p.trans = e->trans; p.start_cdf = e->cdf; p.n_start = (uint32_t)e->eh.cdf.size();
+    p.fixed_start = e->eh.fixed_start;
     p.max_steps = e->eh.max_steps; p.th1 = e->eh.th1; p.th2 = e->eh.th2; p.th3 = e->eh.th3;
     p.trunc_reward = e->eh.trunc_reward;
     // lane init needs aux/epi_reward: use scratch
@@ -645,6 +655,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
     p.trace = a->trace; p.visited = a->visited; p.vis_words = a->vis_words;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
+    p.fixed_start = a->eh.fixed_start;
     p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
     p.trunc_reward = a->eh.trunc_reward;
     p.target_episodes = 0; p.eval_at = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;

@@ -48,6 +48,7 @@ struct KParams {
     const uint32_t *trans; // [S][A] packed
     const double *start_cdf;
     uint32_t n_start;
+    int32_t fixed_start;   // >= 0 when the start distribution is a single state
     uint32_t max_steps;
     double th1, th2, th3;  // slippery FrozenLake cumulative sums
     double trunc_reward;

@@ -120,7 +120,8 @@ template <int ENV>
 __global__ void k_env_reset(KParams p, uint64_t *obs) {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
-    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward};
+    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
+                p.fixed_start};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};
@@ -134,7 +135,8 @@ template <int ENV>
 __global__ void k_env_step(KParams p, const uint32_t *act, uint64_t *obs, double *rew, uint8_t *term) {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
-    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward};
+    EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
+                p.fixed_start};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};

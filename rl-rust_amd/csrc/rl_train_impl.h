@@ -142,17 +142,18 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     L.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;
 }
 
-__device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint64_t lane,
-                                             const LaneRegs &L, bool alive, uint32_t s2, uint32_t a2,
-                                             double r, bool term, double td, uint32_t mode_before) {
+__device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint64_t lane, uint32_t kind,
+                                             uint32_t s, uint32_t a, uint32_t s2, uint32_t a2, double r,
+                                             bool term, double td, uint32_t mode) {
     rl_step_record rec;
-    rec.s = alive ? L.s : 0u;
+    rec.s = s;
     rec.s2 = s2;
-    rec.a = (uint8_t)(alive ? L.a : 0u);
+    rec.a = (uint8_t)a;
     rec.a2 = (uint8_t)a2;
     rec.term = (uint8_t)term;
-    rec.mode = (uint8_t)mode_before;
-    rec.pad = 0;
+    rec.mode = (uint8_t)mode;
+    rec.kind = (uint8_t)kind;
+    rec.pad[0] = rec.pad[1] = rec.pad[2] = 0;
     rec.r = r;
     rec.td = td;
     p.rec[(uint64_t)k * p.L + lane] = rec;
@@ -202,6 +203,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     EnvTables tabs;
     tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+    tabs.fixed_start = p.fixed_start;
 
     const uint64_t lane = (uint64_t)blockIdx.x * p.G + tid;
     const bool active = tid < p.G && lane < p.L;
@@ -261,28 +263,12 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     };
 
     for (uint32_t k = 0; k < p.K; ++k) {
-        // ---------------- R-phase: env.reset() + get_action (src/agent.rs:83-84)
-        const bool doR = L.mode != RL_MODE_DONE && L.need_reset;
-        if (doR) {
-            L.s = E::reset(L.z, L.rng, tabs);
-            L.ready = true;
-            int64_t ra[A], rb[A];
-            load_rows(L.s, ra, rb);
-            L.a = select(L.s, ra, rb);
-            L.need_reset = false;
-            L.epi_reward = 0.0;
-            L.epi_len = 0;
-        }
-        if constexpr (UCB) {
-            if (__syncthreads_or(doR)) {
-                if (doR) atomicAdd(&N[L.s * A + L.a], 1u);
-                const uint32_t c = (uint32_t)__popcll(__ballot(doR));
-                if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
-                __syncthreads();
-            }
-        }
-        // ---------------- S-phase: step + next action (src/agent.rs:88-89)
+        // ---------------- one synchronous step: each live lane either RESETs
+        // (env.reset() + get_action, src/agent.rs:83-84) or STEPs (env.step +
+        // get_action + update, :88-97); one selection per lane per step.
         const bool alive = L.mode != RL_MODE_DONE;
+        const bool doR = alive && L.need_reset;
+        const bool doS = alive && !L.need_reset;
         const uint32_t mode_before = L.mode;
         uint32_t s2 = 0, a2 = 0;
         double r = 0.0;
@@ -290,10 +276,15 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         int64_t ra2[A], rb2[A];
 #pragma unroll
         for (int i = 0; i < A; ++i) { ra2[i] = 0; rb2[i] = 0; }
-        if (alive) {
+        if (doR) {
+            s2 = E::reset(L.z, L.rng, tabs);
+            L.ready = true;
+        } else if (doS) {
             uint32_t pos = L.s;
             E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
+        }
+        if (alive) {
             load_rows(s2, ra2, rb2);
             a2 = select(s2, ra2, rb2);
         }
@@ -306,7 +297,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
-        const bool train = alive && L.mode == RL_MODE_TRAIN;
+        const bool train = doS && L.mode == RL_MODE_TRAIN;
         const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;   // get_values: flag ? alpha : beta
         const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;    // update:     flag ? beta : alpha
         double td = 0.0;
@@ -417,7 +408,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             if (tid == 0) LISTN[0] = 0u;
         }
         __syncthreads();   // Q_{t+1} complete before the next step's reads
-        if (alive) {
+        if (doS) {
             if (train) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
                 if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
@@ -425,10 +416,17 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             } else {
                 L.n_eval++;
             }
-            if (p.rec) write_record(p, k, lane, L, true, s2, a2, r, term, td, mode_before);
+            if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term);
+        } else if (doR) {
+            L.s = s2;
+            L.a = a2;
+            L.need_reset = false;
+            L.epi_reward = 0.0;
+            L.epi_len = 0;
+            if (p.rec) write_record(p, k, lane, 1u, s2, a2, 0u, 0u, 0.0, false, 0.0, mode_before);
         } else if (p.rec && active) {
-            write_record(p, k, lane, L, false, 0, 0, 0.0, false, 0.0, RL_MODE_DONE);
+            write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
         }
     }
 
@@ -489,6 +487,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     EnvTables tabs;
     tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+    tabs.fixed_start = p.fixed_start;
 
     const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
     if (lane >= p.L) return;                 // no barrier after this point
@@ -526,19 +525,21 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     };
 
     for (uint32_t k = 0; k < p.K; ++k) {
-        if (L.mode != RL_MODE_DONE && L.need_reset) {
+        if (L.mode == RL_MODE_DONE) {
+            if (p.rec) write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
+            continue;
+        }
+        if (L.need_reset) {                       // RESET step: src/agent.rs:83-84
             L.s = E::reset(L.z, L.rng, tabs);
             L.ready = true;
             L.a = select(L.s);
             L.need_reset = false;
             L.epi_reward = 0.0;
             L.epi_len = 0;
-        }
-        if (L.mode == RL_MODE_DONE) {
-            if (p.rec) write_record(p, k, lane, L, false, 0, 0, 0.0, false, 0.0, RL_MODE_DONE);
+            if (p.rec) write_record(p, k, lane, 1u, L.s, L.a, 0u, 0u, 0.0, false, 0.0, L.mode);
             continue;
         }
-        const uint32_t mode_before = L.mode;
+        const uint32_t mode_before = L.mode;      // STEP: src/agent.rs:88-101
         uint32_t s2 = 0;
         double r = 0.0;
         bool term = false;
@@ -615,7 +616,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
         } else {
             L.n_eval++;
         }
-        if (p.rec) write_record(p, k, lane, L, true, s2, a2, r, term, td, mode_before);
+        if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
         after_step(p, L, s2, a2, r, term);
     }
     lane_store(p, lane, L);

@@ -37,8 +37,9 @@ class Config(C.Structure):
 
 
 RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
-                         ("term", "u1"), ("mode", "u1"), ("pad", "<u4"),
+                         ("term", "u1"), ("mode", "u1"), ("kind", "u1"), ("pad", "u1", (3,)),
                          ("r", "<f8"), ("td", "<f8")])
+KIND_IDLE, KIND_RESET, KIND_STEP = 0, 1, 2
 assert RECORD_DTYPE.itemsize == 32
 
 

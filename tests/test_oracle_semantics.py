@@ -40,7 +40,7 @@ def test_private_batch_equals_faithful(oracle, env, agent, policy, sel, algo):
         f.train(n, n // 4)
         fr = f.records()
         br = recs[:, lane]
-        br = br[br["mode"] == oracle.MODE_TRAIN]
+        br = br[(br["mode"] == oracle.MODE_TRAIN) & (br["kind"] == oracle.KIND_STEP)]
         assert len(fr) == len(br)
         for k in ("s", "s2", "a", "a2", "term", "r"):
             assert np.array_equal(fr[k], br[k]), k
