@@ -250,8 +250,9 @@ struct rl_agent {
     int64_t *q_base = nullptr;
     uint32_t *qf_base = nullptr, *n_base = nullptr;
     uint64_t *t_base = nullptr;
-    int64_t *delta_own = nullptr, *delta = nullptr;
+    int64_t *delta_own = nullptr, *delta = nullptr, *delta_rep = nullptr;
     uint64_t delta_words = 0;
+    uint32_t n_rep = 1;
     // private
     double *q_priv = nullptr;
     uint32_t *n_priv = nullptr;
@@ -286,13 +287,8 @@ int agent_select_kernel(rl_agent *a) {
     if (a->priv) {
         a->block = dim3(256);
         a->grid = dim3((a->L + 255) / 256);
-        a->smem = 0;
-        // tables only
-        const uint32_t SA = a->S * a->A;
-        size_t s = a->cfg.env.kind != RL_ENV_BLACKJACK ? ((SA * 4 + 15) & ~15u) : 0;
-        if (a->cfg.env.kind == RL_ENV_FROZEN_LAKE || a->cfg.env.kind == RL_ENV_TAXI)
-            s += (a->eh.cdf.size() * 8 + 15) & ~size_t(15);
-        a->smem = s;
+        a->smem = private_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
+                                     a->A, (uint32_t)a->eh.cdf.size());
     } else {
         const uint32_t g = std::min(a->G, a->L);
         a->block = dim3(((g + 63) / 64) * 64);
@@ -380,6 +376,10 @@ int launch_train_kernel(rl_agent *a) {
         HIPC(hipEventRecord(e1, a->stream));
         a->events.emplace_back(e0, e1);
     }
+    if (!a->priv) {                       // fold the group-delta replicas into the delta
+        launch_fold_replicas(a->kp, a->stream);
+        HIPC(hipGetLastError());
+    }
     a->launches++;
     if (a->recording) {
         const size_t n = (size_t)a->K * a->L;
@@ -402,16 +402,25 @@ int launch_apply_kernel(rl_agent *a) {
 }
 
 int run_until_done(rl_agent *a, rl_stats *out) {
-    // stats slot 5 counts lanes that are DONE at the end of a launch
-    for (;;) {
-        HIPC(hipMemsetAsync(&a->stats_d[5], 0, 8, a->stream));
+    // stats slot 5 counts lanes that are DONE at the end of a launch.  Guards: a
+    // lane needs at most (max_steps + 1) steps per episode, so a call that has
+    // not finished after this many launches is a bug, not a long run.
+    const uint64_t max_launches = 1ull << 22;
+    for (uint64_t launch = 0;; ++launch) {
+        if (launch >= max_launches) return fail(RL_E_STATE, "train/evaluate did not finish (launch cap)");
+        if (a->rec_h.size() * sizeof(rl_step_record) > (1ull << 32))
+            return fail(RL_E_OOM, "recorded stream exceeds 4 GiB: record fewer steps");
+        // done-lane counter (slot 5 of every stats replica) is per launch
+        HIPC(hipMemset2DAsync(&a->stats_d[5], 64, 0, 8, STATS_REP, a->stream));
         int rc = launch_train_kernel(a);
         if (rc) return rc;
         rc = launch_apply_kernel(a);
         if (rc) return rc;
-        unsigned long long done = 0;
-        HIPC(hipMemcpyAsync(&done, &a->stats_d[5], 8, hipMemcpyDeviceToHost, a->stream));
+        std::vector<unsigned long long> st(8 * STATS_REP);
+        HIPC(hipMemcpyAsync(st.data(), a->stats_d, st.size() * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
+        unsigned long long done = 0;
+        for (uint32_t r = 0; r < STATS_REP; ++r) done += st[r * 8 + 5];
         if (const char *dump = getenv("RLAMD_DEBUG_LANES")) {   // diagnostics: raw lane records per launch
             std::vector<uint4> c(a->L);
             HIPC(hipMemcpy(c.data(), a->core, a->L * 16, hipMemcpyDeviceToHost));
@@ -618,7 +627,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     a->stream = a->own_stream;
     const size_t L = a->L, SA = (size_t)a->S * a->A, PSA = a->P * SA;
     if ((rc = dalloc(&a->core, L)) || (rc = dalloc(&a->rng, L)) || (rc = dalloc(&a->aux, L)) ||
-        (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, 8)) ||
+        (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, 8 * STATS_REP)) ||
         (rc = dalloc(&a->trans, a->eh.trans.size())) || (rc = dalloc(&a->cdf, a->eh.cdf.size())))
         return bad(rc);
     if (a->priv) {
@@ -632,6 +641,11 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
             return bad(rc);
         a->delta = a->delta_own;
         if (hipMemset(a->delta, 0, a->delta_words * 8) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+        const uint32_t n_groups = (a->L + a->G - 1) / a->G;
+        a->n_rep = std::min<uint32_t>(64u, n_groups);
+        if ((rc = dalloc(&a->delta_rep, a->delta_words * a->n_rep))) return bad(rc);
+        if (hipMemset(a->delta_rep, 0, a->delta_words * a->n_rep * 8) != hipSuccess)
+            return bad(fail(RL_E_HIP, "memset"));
     }
     if (c.agent == RL_AGENT_TRACES) {
         a->vis_words = (a->S + 31) / 32;
@@ -645,13 +659,16 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     if (!a->eh.cdf.empty() &&
         hipMemcpy(a->cdf, a->eh.cdf.data(), a->eh.cdf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         return bad(fail(RL_E_HIP, "table upload"));
-    if (hipMemset(a->stats_d, 0, 64) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+    if (hipMemset(a->stats_d, 0, 64 * STATS_REP) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
 
     KParams &p = a->kp;
     p.L = a->L; p.G = a->G; p.K = a->K; p.S = a->S; p.A = a->A; p.P = a->P;
     p.core = a->core; p.rng = a->rng; p.aux = a->aux; p.epi_reward = a->epi_reward;
     p.q_base = a->q_base; p.qf_base = a->qf_base; p.n_base = a->n_base; p.t_base = a->t_base;
     p.delta = a->delta;
+    p.delta_rep = a->delta_rep;
+    p.n_rep = a->n_rep;
+    p.delta_words = (uint32_t)a->delta_words;
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
     p.trace = a->trace; p.visited = a->visited; p.vis_words = a->vis_words;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
@@ -678,6 +695,7 @@ void rl_agent_destroy(rl_agent *a) {
     for (auto &ev : a->events) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     dfree(a->core); dfree(a->rng); dfree(a->aux); dfree(a->epi_reward);
     dfree(a->q_base); dfree(a->qf_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own);
+    dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->visited); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d);
@@ -777,9 +795,12 @@ int rl_agent_synchronize(rl_agent *a) {
 int rl_agent_stats(rl_agent *a, rl_stats *out) {
     if (!a || !out) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
-    unsigned long long s[8];
-    HIPC(hipMemcpyAsync(s, a->stats_d, 64, hipMemcpyDeviceToHost, a->stream));
+    std::vector<unsigned long long> rep(8 * STATS_REP);
+    HIPC(hipMemcpyAsync(rep.data(), a->stats_d, rep.size() * 8, hipMemcpyDeviceToHost, a->stream));
     HIPC(hipStreamSynchronize(a->stream));
+    unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t r = 0; r < STATS_REP; ++r)
+        for (int i = 0; i < 8; ++i) s[i] += rep[r * 8 + i];
     out->train_steps = s[0];
     out->eval_steps = s[1];
     out->train_episodes = s[2];

@@ -12,6 +12,9 @@ namespace rlamd {
 constexpr int QFRAC = 40;
 // sticky non-finite flags of a fixed-point Q entry (IEEE sum algebra, order free)
 constexpr uint32_t QF_NAN = 1u, QF_PINF = 2u, QF_NINF = 4u;
+// replicas of the u64[8] stats block (same-address atomics from every block
+// serialise; spreading them over replicas removed ~0.3 ms per launch)
+constexpr uint32_t STATS_REP = 64;
 
 // lane core record (uint4, SoA over lanes):
 //   x = s (dense state), y = flags word below, z = env word (curr_step | blackjack hand),
@@ -36,6 +39,9 @@ struct KParams {
     uint32_t *n_base;      // [S][A]
     uint64_t *t_base;      // [1]
     int64_t *delta;        // [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
+    int64_t *delta_rep;    // n_rep replicas of `delta`: group g adds into replica g % n_rep
+    uint32_t n_rep;        // (spreads the same-address int64 atomics of the merge)
+    uint32_t delta_words;
     // private mode (SoA [entry][lane])
     double *q_priv;
     uint32_t *n_priv;
@@ -60,7 +66,7 @@ struct KParams {
     uint32_t eval_episodes;
     int32_t eval_only;
     // outputs
-    unsigned long long *stats; // rl_stats as u64[8]
+    unsigned long long *stats; // rl_stats as u64[8] x STATS_REP replicas (block b adds into b % STATS_REP)
     rl_step_record *rec;       // [K][L] or null
 };
 
@@ -70,6 +76,7 @@ typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, s
 
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
+size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
 
 // env-only kernels (batched Env trait) and KAT probes
 void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs);
@@ -81,6 +88,7 @@ void launch_arm_full(const KParams &p, int32_t mode, uint32_t eval_left, int res
                      hipStream_t s);
 void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s);
 void launch_apply(const KParams &p, int specials, hipStream_t s);
+void launch_fold_replicas(const KParams &p, hipStream_t s);
 void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);
 void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s);
 void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,

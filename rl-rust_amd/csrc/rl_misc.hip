@@ -19,6 +19,10 @@ train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, 
     }
     return nullptr;
 }
+size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start) {
+    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, agent == RL_AGENT_TRACES, S,
+                       A, n_start, 0).total;
+}
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start) {
     return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, agent == RL_AGENT_TRACES, S,
                        A, n_start, 1).total;
@@ -78,6 +82,23 @@ __global__ void k_fill_f64(double *ptr, uint64_t n, double v) {
 }
 void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ptr, n, v);
+}
+
+// ---------------------------------------------------------------- replica fold
+// delta += sum over replicas (exact int64), replicas zeroed for the next launch
+__global__ void k_fold_replicas(KParams p) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= p.delta_words) return;
+    int64_t s = 0;
+    for (uint32_t r = 0; r < p.n_rep; ++r) {
+        int64_t *x = p.delta_rep + (uint64_t)r * p.delta_words + w;
+        s = (int64_t)((uint64_t)s + (uint64_t)*x);
+        *x = 0;
+    }
+    p.delta[w] = (int64_t)((uint64_t)p.delta[w] + (uint64_t)s);
+}
+void launch_fold_replicas(const KParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_fold_replicas, dim3((p.delta_words + 255) / 256), dim3(256), 0, s, p);
 }
 
 // ---------------------------------------------------------------- merge apply

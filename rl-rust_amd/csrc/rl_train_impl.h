@@ -18,7 +18,7 @@
 namespace rlamd {
 
 struct SmemLayout {
-    uint32_t q, sum, cnt, qf, n, t, list, tr, cdf, total;
+    uint32_t st, q, sum, cnt, qf, n, t, list, tr, cdf, total;
 };
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 // LDS carve of one learner group (shared mode) or of the tables only (private).
@@ -32,6 +32,7 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     SmemLayout l;
     const uint32_t SA = S * A, PSA = (uint32_t)P * SA;
     uint32_t off = 0;
+    l.st = off; off += 64u;                       // per-block stats accumulators (u64[8])
     l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.cnt = off; off += shared_q ? align16(((PSA + 1u) / 2u) * 4u) : 0u;
@@ -96,15 +97,21 @@ __device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, cons
     p.epi_reward[lane] = L.epi_reward;
 }
 
-// per-launch counters -> rl_stats (one atomic per wave per counter)
-__device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, bool active) {
+// per-launch counters -> rl_stats: wave sums -> block sums in LDS -> one
+// atomic per block and counter into stats replica blockIdx % STATS_REP.
+// Every thread of the block must call this (it contains barriers).
+__device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, bool active,
+                                            unsigned long long *acc) {
     const uint64_t v[6] = {L.n_train, L.n_eval, L.n_tep, L.n_eep, (uint64_t)L.rsum,
                            (uint64_t)(active && L.mode == RL_MODE_DONE)};
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int64_t s = wave_sum_i64((int64_t)v[i]);
-        if ((threadIdx.x & 63u) == 0 && s != 0) atomicAdd(&p.stats[i], (unsigned long long)s);
+        if ((threadIdx.x & 63u) == 0 && s != 0) atomicAdd(&acc[i], (unsigned long long)s);
     }
+    __syncthreads();
+    if (threadIdx.x < 6 && acc[threadIdx.x])
+        atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * 8u + threadIdx.x], acc[threadIdx.x]);
 }
 
 // bookkeeping after the update: src/agent.rs:98-116 + the eval interleave.
@@ -185,7 +192,9 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
 
+    unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    if (tid < 8) ACC[tid] = 0ull;
     for (uint32_t i = tid; i < PSA; i += nthr) { Q[i] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
     for (uint32_t i = tid; i < (PSA + 1u) / 2u; i += nthr) CNT[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
@@ -431,29 +440,31 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     }
 
     if (active) lane_store(p, lane, L);
-    flush_stats(p, L, active);
+    flush_stats(p, L, active, ACC);
 
     // ---------------- emit this group's ΔQ (and ΔN, Δt, new flags) for the merge
-    // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts]
+    // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts],
+    // into replica blockIdx % n_rep (folded by k_fold_replicas)
+    int64_t *const dl = p.delta_rep + (uint64_t)(blockIdx.x % p.n_rep) * p.delta_words;
     __syncthreads();
     for (uint32_t i = tid; i < PSA; i += nthr) {
         const int64_t d = (int64_t)(Q[i] - (unsigned long long)p.q_base[i]);
         if (d) {
-            atomicAdd((unsigned long long *)&p.delta[i], (unsigned long long)d);
-            atomicAdd((unsigned long long *)&p.delta[PSA + i], 1ull);
+            atomicAdd((unsigned long long *)&dl[i], (unsigned long long)d);
+            atomicAdd((unsigned long long *)&dl[PSA + i], 1ull);
         }
     }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < SA; i += nthr) {
             const int64_t d = (int64_t)N[i] - (int64_t)p.n_base[i];
-            if (d) atomicAdd((unsigned long long *)&p.delta[2 * PSA + i], (unsigned long long)d);
+            if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + i], (unsigned long long)d);
         }
         if (tid == 0) {
             const int64_t d = (int64_t)(T[0] - p.t_base[0]);
-            if (d) atomicAdd((unsigned long long *)&p.delta[2 * PSA + SA], (unsigned long long)d);
+            if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + SA], (unsigned long long)d);
         }
         if constexpr (SPEC) {
-            int64_t *fc = p.delta + 2 * PSA + SA + 1;
+            int64_t *fc = dl + 2 * PSA + SA + 1;
             for (uint32_t i = tid; i < PSA; i += nthr) {
                 const uint32_t nf = QF8[i] & ~p.qf_base[i];
                 if (nf & QF_NAN) atomicAdd((unsigned long long *)&fc[i], 1ull);
@@ -466,6 +477,10 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 
 // ======================================================================== private
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
+                                                 LaneRegs &L);
+
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -477,7 +492,9 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES, S, A, p.n_start, 0);
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
+    unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    if (tid < 8) ACC[tid] = 0ull;
     if constexpr (ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
     if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_TAXI)
@@ -490,9 +507,22 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     tabs.fixed_start = p.fixed_start;
 
     const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
-    if (lane >= p.L) return;                 // no barrier after this point
+    const bool active = lane < p.L;
     LaneRegs L;
-    lane_load(p, lane, true, L);
+    lane_load(p, lane, active, L);
+    if (active) run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L);
+    flush_stats(p, L, active, ACC);
+}
+
+// one private lane (a whole reference agent) for K synchronous steps
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
+                                                 LaneRegs &L) {
+    using E = EnvDev<ENV>;
+    constexpr int A = E::A;
+    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    constexpr bool UCB = SEL == RL_SEL_UCB;
+    const uint32_t SA = p.S * (uint32_t)A;
     const uint64_t Ls = p.L;
     uint64_t t = UCB ? p.t_priv[lane] : 0;
 
@@ -621,12 +651,6 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     }
     lane_store(p, lane, L);
     if (UCB) p.t_priv[lane] = t;
-    // stats without wave reductions (inactive lanes returned early)
-    const uint64_t v[6] = {L.n_train, L.n_eval, L.n_tep, L.n_eep, (uint64_t)L.rsum,
-                           (uint64_t)(L.mode == RL_MODE_DONE)};
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-        if (v[i]) atomicAdd(&p.stats[i], (unsigned long long)v[i]);
 }
 
 // ---------------------------------------------------------------- launch table
