@@ -962,12 +962,14 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
 
 /* The shared-mode combination rule: an entry moves by the MEAN of the n
  * contributions it received (this step's lanes, or the groups that changed it
- * at a merge).  n == 1 is exact (so one lane reproduces the reference update);
- * n > 1 divides in f64 and truncates toward zero — both correctly rounded
- * IEEE operations, so host and gfx950 agree bit for bit. */
+ * at a merge): trunc((double)sum * (1.0/n)), with 1.0/n correctly rounded.
+ * n == 1 is exact (|sum| <= 2^53, so one lane reproduces the reference update);
+ * n == 0 has sum == 0.  Conversions, the reciprocal and the product are
+ * correctly rounded IEEE operations, so host and gfx950 agree bit for bit (the
+ * device reads 1.0/n from a table, rlamd rl_train_impl.h mean_delta). */
 static int64_t mean_delta(int64_t sum, int64_t n) {
-    if (n <= 1) return n == 1 ? sum : 0;
-    return (int64_t)trunc((double)sum / (double)n);
+    if (n <= 0) return 0;
+    return (int64_t)trunc((double)sum * (1.0 / (double)n));
 }
 
 /* One synchronous step of a learner group.  Every live lane does exactly one

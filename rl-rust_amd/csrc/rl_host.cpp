@@ -294,7 +294,7 @@ int agent_select_kernel(rl_agent *a) {
         a->block = dim3(((g + 63) / 64) * 64);
         a->grid = dim3((a->L + a->G - 1) / a->G);
         a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
-                                    a->A, (uint32_t)a->eh.cdf.size());
+                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x);
         if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
     }
     return RL_OK;
@@ -675,7 +675,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.fixed_start = a->eh.fixed_start;
     p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
     p.trunc_reward = a->eh.trunc_reward;
-    p.target_episodes = 0; p.eval_at = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;
+    p.target_episodes = 0; p.eval_at = 0; p.eval_div = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;
     p.stats = a->stats_d;
     p.rec = nullptr;
     agent_sync_params(a);
@@ -746,6 +746,7 @@ int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats 
     }
     a->kp.target_episodes = n_episodes;
     a->kp.eval_at = eval_at;
+    a->kp.eval_div = eval_at ? ~0ull / eval_at + 1ull : 0ull;   // eval_hit() in rl_train_impl.h
     a->kp.eval_only = 0;
     int rc = run_until_done(a, out);
     a->kp.target_episodes = 0;

@@ -63,6 +63,7 @@ struct KParams {
     int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
     // train()/evaluate() control
     uint64_t target_episodes, eval_at;
+    uint64_t eval_div;     // ceil(2^64 / eval_at) (mod 2^64): divisibility test constant
     uint32_t eval_episodes;
     int32_t eval_only;
     // outputs
@@ -75,7 +76,8 @@ typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, s
                                       hipStream_t stream);
 
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
-size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
+size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start,
+                         uint32_t nthr);
 size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
 
 // env-only kernels (batched Env trait) and KAT probes

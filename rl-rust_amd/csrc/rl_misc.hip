@@ -21,11 +21,12 @@ train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, 
 }
 size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start) {
     return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, agent == RL_AGENT_TRACES, S,
-                       A, n_start, 0).total;
+                       A, n_start, 0u).total;
 }
-size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start) {
+size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start,
+                         uint32_t nthr) {
     return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, agent == RL_AGENT_TRACES, S,
-                       A, n_start, 1).total;
+                       A, n_start, nthr).total;
 }
 
 // ---------------------------------------------------------------- lane init

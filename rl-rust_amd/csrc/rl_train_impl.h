@@ -18,7 +18,7 @@
 namespace rlamd {
 
 struct SmemLayout {
-    uint32_t st, q, sum, cnt, qf, n, t, list, tr, cdf, total;
+    uint32_t st, q, sum, cnt, qf, n, t, list, rcp, tr, cdf, total;
 };
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 // LDS carve of one learner group (shared mode) or of the tables only (private).
@@ -26,9 +26,13 @@ __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15
 //   sum  int64 [P][S][A]   this step's summed deltas per entry
 //   cnt  u16   [P][S][A]   this step's contributions per entry (u32-word atomics)
 //   qf   u8    [P][S][A]   sticky non-finite flags (UCB + expected SARSA only)
-//   n/t  UCB counters;  list u16 touched entries + count (traces);  tr/cdf env tables
+//   n/t  UCB counters;  list u16 touched entries + count (traces)
+//   rcp  f64 [nthr+1]   1.0/n for the combination rule (mean_delta)
+//   tr/cdf env tables
+// nthr = the shared kernel's block size; 0 for the private kernel (tables only).
 __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int traces, uint32_t S,
-                                                  uint32_t A, uint32_t n_start, int shared_q) {
+                                                  uint32_t A, uint32_t n_start, uint32_t nthr) {
+    const int shared_q = nthr != 0;
     SmemLayout l;
     const uint32_t SA = S * A, PSA = (uint32_t)P * SA;
     uint32_t off = 0;
@@ -40,6 +44,7 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.n = off; off += (shared_q && ucb) ? align16(SA * 4u) : 0u;
     l.t = off; off += (shared_q && ucb) ? 16u : 0u;
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
+    l.rcp = off; off += shared_q ? align16((nthr + 1u) * 8u) : 0u;
     l.tr = off; off += env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
     l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_TAXI) ? align16(n_start * 8u) : 0u;
     l.total = off;
@@ -47,11 +52,17 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
 }
 
 // The shared-mode combination rule (oracle: rlref.c mean_delta): an entry moves
-// by the MEAN of the n contributions it received; n == 1 is exact, n > 1 is an
-// f64 divide + truncation (correctly rounded on host and gfx950 alike).
+// by the MEAN of the n contributions it received, trunc((double)sum * (1.0/n))
+// with 1.0/n correctly rounded (rcp[0] = 0, rcp[1] = 1: n <= 1 is exact).
+// The device form reads 1.0/n from the LDS table and converts with the
+// 1.5*2^52 magic add (|mean| <= 2^51 for step contributions).
 __host__ __device__ inline int64_t mean_delta(int64_t sum, int64_t n) {
-    if (n <= 1) return n == 1 ? sum : 0;
-    return (int64_t)__builtin_trunc((double)sum / (double)n);
+    if (n <= 0) return 0;
+    return (int64_t)__builtin_trunc((double)sum * (1.0 / (double)n));
+}
+__device__ __forceinline__ int64_t mean_delta_rcp(int64_t sum, double rcp) {
+    const double y = __builtin_trunc((double)sum * rcp) + 0x1.8p52;
+    return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
 }
 
 // ---------------------------------------------------------------- lane state
@@ -61,9 +72,12 @@ struct LaneRegs {
     uint32_t mode;
     bool need_reset, ready, dflag;
     double eps, epi_reward;
-    // per-launch counters
-    uint32_t n_train, n_eval, n_tep, n_eep;
-    int64_t rsum;
+};
+// per-launch counters (rl_stats slots 0-4); the shared kernel keeps them per
+// wave in scalar registers (ballot counts), the private kernel per lane
+struct Counters {
+    uint32_t n_train = 0, n_eval = 0, n_tep = 0, n_eep = 0;
+    int64_t rsum = 0;      // sum over finished training episodes of rint(reward * 2^16)
 };
 
 __device__ __forceinline__ void lane_load(const KParams &p, uint64_t lane, bool active, LaneRegs &L) {
@@ -83,8 +97,6 @@ __device__ __forceinline__ void lane_load(const KParams &p, uint64_t lane, bool 
     L.eval_left = x.z;
     L.epi_len = x.w;
     L.epi_reward = er;
-    L.n_train = L.n_eval = L.n_tep = L.n_eep = 0;
-    L.rsum = 0;
 }
 __device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, const LaneRegs &L) {
     const uint32_t y = (L.a & LF_ACT_MASK) | (L.need_reset ? LF_NEED_RESET : 0u) |
@@ -97,29 +109,39 @@ __device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, cons
     p.epi_reward[lane] = L.epi_reward;
 }
 
-// per-launch counters -> rl_stats: wave sums -> block sums in LDS -> one
+// per-launch counters -> rl_stats: wave sums -> block sums in LDS (acc) -> one
 // atomic per block and counter into stats replica blockIdx % STATS_REP.
-// Every thread of the block must call this (it contains barriers).
-__device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, bool active,
-                                            unsigned long long *acc) {
-    const uint64_t v[6] = {L.n_train, L.n_eval, L.n_tep, L.n_eep, (uint64_t)L.rsum,
+// Every thread of the block must call these (they contain a barrier).
+__device__ __forceinline__ void flush_block(const KParams &p, unsigned long long *acc) {
+    __syncthreads();
+    if (threadIdx.x < 6 && acc[threadIdx.x])
+        atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * 8u + threadIdx.x], acc[threadIdx.x]);
+}
+__device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, const Counters &C,
+                                            bool active, unsigned long long *acc) {
+    const uint64_t v[6] = {C.n_train, C.n_eval, C.n_tep, C.n_eep, (uint64_t)C.rsum,
                            (uint64_t)(active && L.mode == RL_MODE_DONE)};
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int64_t s = wave_sum_i64((int64_t)v[i]);
         if ((threadIdx.x & 63u) == 0 && s != 0) atomicAdd(&acc[i], (unsigned long long)s);
     }
-    __syncthreads();
-    if (threadIdx.x < 6 && acc[threadIdx.x])
-        atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * 8u + threadIdx.x], acc[threadIdx.x]);
+    flush_block(p, acc);
+}
+// 1 when the episode index is a multiple of eval_at (src/agent.rs:107):
+// Lemire's divisibility test, ep * c <= c - 1 (mod 2^64) with c = ceil(2^64 / eval_at)
+// precomputed on the host (eval_div; 0 for eval_at == 1, every episode).
+__device__ __forceinline__ bool eval_hit(const KParams &p, uint32_t ep) {
+    return p.eval_at != 0 && (uint64_t)ep * p.eval_div <= p.eval_div - 1ull;
 }
 
 // bookkeeping after the update: src/agent.rs:98-116 + the eval interleave.
 // Written as predicated selects (no divergent branches): lanes end episodes at
 // different steps, and the branchy form was mis-scheduled at -O3 (a lost
 // train_ep increment, caught by the parity tests).
+// Sets tr / ev when a training / evaluation episode ended (the caller counts them).
 __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32_t s2, uint32_t a2,
-                                           double r, bool term) {
+                                           double r, bool term, bool &tr_out, bool &ev_out) {
     L.epi_reward += r;
     L.epi_len += 1;
     L.s = s2;
@@ -128,9 +150,7 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     const bool ev = term && L.mode == RL_MODE_EVAL;
     const uint32_t ep = L.train_ep;                      // index of the episode that just ended
     const uint32_t new_ep = ep + (tr ? 1u : 0u);
-    bool hit = false;                                    // episode % eval_at == 0 (src/agent.rs:107)
-    if (p.eval_at) hit = ((uint64_t)ep % p.eval_at) == 0;
-    const bool go_eval = tr && hit && p.eval_episodes != 0;
+    const bool go_eval = tr && p.eval_episodes != 0 && eval_hit(p, ep);   // episode % eval_at == 0
     const bool reached = p.target_episodes != 0 && (uint64_t)new_ep >= p.target_episodes;
     const bool tr_done = tr && !go_eval && reached;
     const uint32_t el = L.eval_left - (ev ? 1u : 0u);
@@ -144,9 +164,8 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     L.train_ep = new_ep;
     L.eval_left = go_eval ? p.eval_episodes : el;
     L.need_reset = L.need_reset || term;
-    L.n_tep += tr ? 1u : 0u;
-    L.n_eep += ev ? 1u : 0u;
-    L.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;
+    tr_out = tr;
+    ev_out = ev;
 }
 
 __device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint64_t lane, uint32_t kind,
@@ -178,7 +197,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES, S, A, p.n_start, 1);
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES, S, A, p.n_start, nthr);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // two u16 counters per word
@@ -191,10 +211,11 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSA * 2u));
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
+    double *RCP = (double *)(smem + lay.rcp);
 
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
-    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     if (tid < 8) ACC[tid] = 0ull;
+    for (uint32_t i = tid; i <= nthr; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
     for (uint32_t i = tid; i < PSA; i += nthr) { Q[i] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
     for (uint32_t i = tid; i < (PSA + 1u) / 2u; i += nthr) CNT[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
@@ -253,23 +274,31 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             return argmax<A>(u);
         }
     };
-    // add n contributions summing to `sum` to entry idx; true for the step's first
-    // contributor, which owns the entry in the settle phase
+    // add n contributions summing to `sum` to entry idx.  Sweep form (the table
+    // fits the block, PSA <= nthr): thread i settles entry i every step, so the
+    // counter add needs no return value.  Owner form: the step's first
+    // contributor (old count 0) settles the entry.
+    const bool sweep = PSA <= nthr;
     auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
         const uint32_t sh = (idx & 1u) * 16u;
-        const uint32_t old = atomicAdd(&CNT[idx >> 1], n << sh);
+        bool first = false;
+        if (sweep) atomicAdd(&CNT[idx >> 1], n << sh);
+        else first = ((atomicAdd(&CNT[idx >> 1], n << sh) >> sh) & 0xffffu) == 0u;
         if (sum) atomicAdd(&SUM[idx], (unsigned long long)sum);
         if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
-        return ((old >> sh) & 0xffffu) == 0u;
+        return first;
     };
     // owner: Q[idx] += mean of the step's contributions (clamped), clear accumulators
     auto settle = [&](uint32_t idx) {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
-        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta(sum, (int64_t)n));
+        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, RCP[n]));
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
     };
+    // wave-level per-launch counters (scalar registers: ballot popcounts)
+    uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
+    unsigned long long *const RSUM = &ACC[4];
 
     for (uint32_t k = 0; k < p.K; ++k) {
         // ---------------- one synchronous step: each live lane either RESETs
@@ -283,8 +312,6 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         double r = 0.0;
         bool term = false;
         int64_t ra2[A], rb2[A];
-#pragma unroll
-        for (int i = 0; i < A; ++i) { ra2[i] = 0; rb2[i] = 0; }
         if (doR) {
             s2 = E::reset(L.z, L.rng, tabs);
             L.ready = true;
@@ -293,10 +320,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
-        if (alive) {
-            load_rows(s2, ra2, rb2);
-            a2 = select(s2, ra2, rb2);
-        }
+        load_rows(s2, ra2, rb2);                   // s2 == 0 (a valid row) on idle lanes
+        if (alive) a2 = select(s2, ra2, rb2);
         if constexpr (UCB) {
             __syncthreads();
             if (alive) atomicAdd(&N[s2 * A + a2], 1u);
@@ -353,7 +378,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                 owner = contribute(idx, dq, 1u, fl);
             }
             __syncthreads();   // all contributions in, all Q reads done
-            if (owner) settle(idx);
+            if (sweep) { if (tid < PSA) settle(tid); }
+            else if (owner) settle(idx);
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda.  Per-lane deltas
@@ -392,7 +418,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                             if constexpr (SPEC) f = wave_or_u32(mine_t ? fl : 0u);
                             const uint32_t idx = (uint32_t)t * SA + o * A + b;
                             if ((tid & 63u) == 0 && n) {
-                                if (contribute(idx, sum, n, f)) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
+                                if (contribute(idx, sum, n, f) && !sweep)
+                                    LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
                             }
                         }
                     }
@@ -411,22 +438,25 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                 }
             }
             __syncthreads();   // all contributions in, all Q reads done
-            const uint32_t n_touched = LISTN[0];
-            for (uint32_t i = tid; i < n_touched; i += nthr) settle(LIST[i]);
-            __syncthreads();
-            if (tid == 0) LISTN[0] = 0u;
+            if (sweep) {
+                if (tid < PSA) settle(tid);
+            } else {
+                const uint32_t n_touched = LISTN[0];
+                for (uint32_t i = tid; i < n_touched; i += nthr) settle(LIST[i]);
+                __syncthreads();
+                if (tid == 0) LISTN[0] = 0u;
+            }
         }
         __syncthreads();   // Q_{t+1} complete before the next step's reads
+        bool tr = false, ev = false;
         if (doS) {
             if (train) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
                 if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
-                L.n_train++;
-            } else {
-                L.n_eval++;
             }
             if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
-            after_step(p, L, s2, a2, r, term);
+            after_step(p, L, s2, a2, r, term, tr, ev);
+            if (tr) atomicAdd(RSUM, (unsigned long long)(int64_t)__builtin_rint(L.epi_reward * 65536.0));
         } else if (doR) {
             L.s = s2;
             L.a = a2;
@@ -437,10 +467,24 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
         } else if (p.rec && active) {
             write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
         }
+        c_train += (uint32_t)__popcll(__ballot(train));
+        c_eval += (uint32_t)__popcll(__ballot(doS && !train));
+        c_tep += (uint32_t)__popcll(__ballot(tr));
+        c_eep += (uint32_t)__popcll(__ballot(ev));
     }
 
     if (active) lane_store(p, lane, L);
-    flush_stats(p, L, active, ACC);
+    {
+        const uint32_t c_done = (uint32_t)__popcll(__ballot(active && L.mode == RL_MODE_DONE));
+        if ((tid & 63u) == 0) {
+            if (c_train) atomicAdd(&ACC[0], (unsigned long long)c_train);
+            if (c_eval) atomicAdd(&ACC[1], (unsigned long long)c_eval);
+            if (c_tep) atomicAdd(&ACC[2], (unsigned long long)c_tep);
+            if (c_eep) atomicAdd(&ACC[3], (unsigned long long)c_eep);
+            if (c_done) atomicAdd(&ACC[5], (unsigned long long)c_done);
+        }
+        flush_block(p, ACC);
+    }
 
     // ---------------- emit this group's ΔQ (and ΔN, Δt, new flags) for the merge
     // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts],
@@ -478,7 +522,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // ======================================================================== private
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
-                                                 LaneRegs &L);
+                                                 LaneRegs &L, Counters &C);
 
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(256) k_train_private(KParams p) {
@@ -489,7 +533,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     const uint32_t S = p.S, SA = S * (uint32_t)A;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES, S, A, p.n_start, 0);
+    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES, S, A, p.n_start, 0u);
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
@@ -509,15 +553,16 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
     const bool active = lane < p.L;
     LaneRegs L;
+    Counters C;
     lane_load(p, lane, active, L);
-    if (active) run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L);
-    flush_stats(p, L, active, ACC);
+    if (active) run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L, C);
+    flush_stats(p, L, C, active, ACC);
 }
 
 // one private lane (a whole reference agent) for K synchronous steps
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
-                                                 LaneRegs &L) {
+                                                 LaneRegs &L, Counters &C) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
     constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
@@ -642,12 +687,16 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             }
             if (P == 2) L.dflag = !L.dflag;
             if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
-            L.n_train++;
+            C.n_train++;
         } else {
-            L.n_eval++;
+            C.n_eval++;
         }
         if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
-        after_step(p, L, s2, a2, r, term);
+        bool tr, ev;
+        after_step(p, L, s2, a2, r, term, tr, ev);
+        C.n_tep += tr ? 1u : 0u;
+        C.n_eep += ev ? 1u : 0u;
+        C.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;
     }
     lane_store(p, lane, L);
     if (UCB) p.t_priv[lane] = t;

@@ -39,8 +39,15 @@ if "GRBM_GUI_ACTIVE" in m:
     if "SQ_INSTS_VALU" in m:
         # 256 CUs x 4 SIMDs; a wave64 VALU op occupies a SIMD32 for 2 cycles
         out["valu_busy_frac"] = m["SQ_INSTS_VALU"] * 2 / (cyc * 256 * 4)
+    if "SQ_LDS_IDX_ACTIVE" in m:
+        out["lds_active_frac"] = m["SQ_LDS_IDX_ACTIVE"] / 256 / cyc
     if "SQ_LDS_BANK_CONFLICT" in m:
         out["lds_bank_conflict_cycles_per_cu"] = m["SQ_LDS_BANK_CONFLICT"] / 256
+if "SQ_WAVE_CYCLES" in m:
+    w = m["SQ_WAVE_CYCLES"]
+    out["wave_cycle_split"] = {k: m[k] / w for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                      "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VALU",
+                                                      "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA") if k in m}
 out["kernel_avg_ns"] = t_ns
 json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
