@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """bench.py — training env-steps/s of the MI355X hot path.
 
-Workload (BASELINE.json configs[1]): FrozenLake-8x8 (deterministic), one-step
-Q-learning, eps-greedy, 2^20 lanes per GPU, learner groups of 256 lanes
-(one workgroup, Q in LDS), merge every K=64 synchronous steps.
-One bench "step" = one launch = K synchronous env-steps of every lane + the
-merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).
+Workload (BASELINE.json configs[1] = SURVEY §8(d) cfg 2): FrozenLake-8x8
+(deterministic), one-step Q-learning, eps-greedy, 2^20 lanes per GPU, learner
+groups of 256 lanes (one workgroup, Q in LDS), merge every K=64 synchronous
+steps.  One bench "step" = one launch = K synchronous env-steps of every lane +
+the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
+§8(d): warm-up 64 synchronous steps (1 launch), timed window 4,096 (64 launches).
+--config 3/4/5 selects the other §8(d) workloads (per-GPU lane counts).
 
   python bench.py [--gpus N --steps K --warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -33,22 +35,38 @@ HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--lanes", type=int, default=1 << 20, help="env lanes per GPU")
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="SURVEY §8(d) workload preset (2 = the headline)")
+    ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU")
     ap.add_argument("--group", type=int, default=256)
     ap.add_argument("--sync", type=int, default=64, help="K: synchronous steps per launch")
-    ap.add_argument("--env", default="frozen_lake")
+    for k in ("env", "agent", "policy", "selector", "algo"):
+        ap.add_argument("--" + k, default=None)
     ap.add_argument("--map8x8", type=int, default=1)
     ap.add_argument("--slippery", type=int, default=0)
-    ap.add_argument("--agent", default="one_step")
-    ap.add_argument("--policy", default="tabular")
-    ap.add_argument("--selector", default="eps_greedy")
-    ap.add_argument("--algo", default="qlearning")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
+
+
+# SURVEY §8(d) workloads; lanes are per GPU (cfg 4: 2^19 over 4 GPUs, cfg 5: 2^22 over 8)
+PRESETS = {
+    2: dict(env="frozen_lake", agent="one_step", policy="tabular", selector="eps_greedy",
+            algo="qlearning", lanes=1 << 20),
+    3: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="expected_sarsa",
+            lanes=1 << 20),
+    4: dict(env="cliff_walking", agent="traces", policy="tabular", selector="eps_greedy", algo="sarsa",
+            lanes=1 << 17),
+    5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
+            lanes=1 << 19),
+}
 
 
 def cpu_baseline(args):
@@ -64,9 +82,9 @@ def cpu_baseline(args):
     selk = {"eps_greedy": 0, "ucb": 1}[args.selector]
     algok = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}[args.algo]
 
-    def run(n):
+    def run(n, threads=1):
         out = subprocess.run([exe, str(envk), str(args.map8x8), str(args.slippery), str(agentk),
-                              str(polk), str(selk), str(algok), str(n), "0", "1"],
+                              str(polk), str(selk), str(algok), str(n), "0", str(threads)],
                              check=True, capture_output=True, text=True).stdout
         return json.loads(out)
 
@@ -75,11 +93,20 @@ def cpu_baseline(args):
     eps_per_sec = 20000 / max(probe["seconds"], 1e-6)
     n = max(20000, int(eps_per_sec * args.cpu_seconds))
     r = run(n)
-    return {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle faithful single-env loop (src/agent.rs:66-118 restated in C), "
-                      f"{args.env} {'8x8' if args.map8x8 else '4x4'} {args.agent} {args.algo} "
-                      f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s "
-                      f"(probe {rate:.3g} steps/s)"}
+    res = {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"oracle faithful single-env loop (src/agent.rs:66-118 restated in C), "
+                     f"{args.env} {'8x8' if args.map8x8 else '4x4'} {args.agent} {args.algo} "
+                     f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s "
+                     f"(probe {rate:.3g} steps/s)"}
+    # one independent faithful env per host core (the box's CPU
+    # share is 16 threads; os.cpu_count() reports the whole machine)
+    threads = min(16, os.cpu_count() or 1)
+    if threads > 1:
+        m = run(max(20000, int(eps_per_sec * args.cpu_seconds / 4)), threads)   # episodes per thread
+        res["multi_core"] = {"value": m["steps_per_sec"], "cores": threads,
+                             "sample": f"{threads} independent faithful envs, {m['steps']} env-steps "
+                                       f"in {m['seconds']:.2f} s"}
+    return res
 
 
 def main():
@@ -158,7 +185,8 @@ def main():
     if os.path.exists(args.traffic_file):
         try:
             tf = json.load(open(args.traffic_file))
-            if tf.get("lanes") == args.lanes and tf.get("sync") == args.sync and tf.get("env") == args.env:
+            if (tf.get("lanes") == args.lanes and tf.get("sync") == args.sync and tf.get("env") == args.env
+                    and tf.get("group") == args.group and tf.get("algo") == args.algo):
                 traffic = tf.get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
@@ -170,7 +198,7 @@ def main():
         "config": {"workload": f"{args.env} {'8x8' if args.map8x8 else '4x4'}"
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
-                   "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
+                   "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,

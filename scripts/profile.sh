@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 R=${ROUND:-r01}
 O=gpurun_out/prof_$R
 mkdir -p $O
-B="bench.py --no-cpu-baseline --steps 20 --warmup 5 ${BENCH_ARGS}"
+B="bench.py --no-cpu-baseline ${BENCH_ARGS}"   # the bench defaults: the same command the driver times
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $B > $O/trace.log 2>&1 || exit $?
 PASSES=${PASSES:-"FETCH_SIZE WRITE_SIZE SQ_WAVES_SQ_INSTS_VALU_SQ_INSTS_LDS_SQ_INSTS_SALU SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_SQ_WAIT_INST_LDS_SQ_ACTIVE_INST_VALU_SQ_ACTIVE_INST_LDS_SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE_SQ_LDS_BANK_CONFLICT_SQ_LDS_IDX_ACTIVE_SQ_INSTS_VMEM_RD_SQ_INSTS_VMEM_WR"}
 for n in $PASSES; do
