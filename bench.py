@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="SURVEY §8(d) workload preset (2 = the headline)")
     ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU")
-    ap.add_argument("--group", type=int, default=256)
+    ap.add_argument("--group", type=int, default=None, help="learner-group size (lanes per workgroup)")
     ap.add_argument("--sync", type=int, default=64, help="K: synchronous steps per launch")
     for k in ("env", "agent", "policy", "selector", "algo"):
         ap.add_argument("--" + k, default=None)
@@ -59,13 +59,13 @@ def parse():
 # SURVEY §8(d) workloads; lanes are per GPU (cfg 4: 2^19 over 4 GPUs, cfg 5: 2^22 over 8)
 PRESETS = {
     2: dict(env="frozen_lake", agent="one_step", policy="tabular", selector="eps_greedy",
-            algo="qlearning", lanes=1 << 20),
+            algo="qlearning", lanes=1 << 20, group=256),
     3: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="expected_sarsa",
-            lanes=1 << 20),
+            lanes=1 << 20, group=1024),
     4: dict(env="cliff_walking", agent="traces", policy="tabular", selector="eps_greedy", algo="sarsa",
-            lanes=1 << 17),
+            lanes=1 << 17, group=256),
     5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
-            lanes=1 << 19),
+            lanes=1 << 19, group=1024),
 }
 
 
@@ -179,7 +179,12 @@ def main():
         total_steps = steps_done
     value = total_steps / wall
     avg_kern_s = kern_ms / max(n_kern, 1) / 1e3
-    bytes_per_launch = BYTES_PER_STEP * steps_done / args.steps      # env-steps per launch x 32 B
+    # 32 B per env-step; traces add (16*A + 2) B per visited state
+    # swept (f64 trace read + write per action, u16 slot id), V-bar counted on the device
+    n_act = {"frozen_lake": 4, "cliff_walking": 4, "taxi": 6, "blackjack": 2}[args.env]
+    v_bar = (st1["trace_states"] - st0["trace_states"]) / max(steps_done, 1)
+    bytes_per_step = BYTES_PER_STEP + (16 * n_act + 2) * v_bar
+    bytes_per_launch = bytes_per_step * steps_done / args.steps
     achieved = bytes_per_launch / avg_kern_s
     traffic = None
     if os.path.exists(args.traffic_file):
@@ -195,7 +200,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (env lanes seeded per global lane id; no dataset)",
-        "config": {"workload": f"{args.env} {'8x8' if args.map8x8 else '4x4'}"
+        "config": {"workload": f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
                    "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
@@ -206,7 +211,8 @@ def main():
                      "traffic": traffic,
                      "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
                      "kernel_launches": n_kern,
-                     "bytes_per_launch": bytes_per_launch},
+                     "bytes_per_launch": bytes_per_launch, "bytes_per_env_step": bytes_per_step,
+                     **({"trace_v_bar": v_bar} if args.agent == "traces" else {})},
         "torch_event_ms": ev0.elapsed_time(ev1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

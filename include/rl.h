@@ -111,7 +111,8 @@ typedef struct rl_stats {
     int64_t reward_sum_q16;   /* sum of training-episode rewards, fixed point 2^-16 */
     uint64_t done_lanes;      /* lanes that finished the current train()/evaluate() call */
     uint64_t launches;
-    uint64_t reserved;
+    uint64_t trace_states;    /* traces agents: sum over training steps of the visited-set size
+                                 swept by the eligibility update (mean = V-bar of SURVEY 8(d)) */
 } rl_stats;
 
 typedef struct rl_env rl_env;

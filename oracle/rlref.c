@@ -1048,6 +1048,7 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
                 L->visited[s] = 1;
                 for (uint32_t o = 0; o < b->S; ++o) {
                     if (!L->visited[o]) continue;
+                    b->stats[7]++;                    /* visited-set entries swept (V per step) */
                     for (uint32_t bb = 0; bb < A; ++bb) {
                         double *e = &L->trace[(size_t)o * A + bb];
                         add_delta(b, ut, o, bb, b->c.lr * (td * *e));

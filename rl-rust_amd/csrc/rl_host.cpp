@@ -259,8 +259,8 @@ struct rl_agent {
     uint64_t *t_priv = nullptr;
     // traces
     double *trace = nullptr;
-    uint32_t *visited = nullptr;
-    uint32_t vis_words = 0;
+    uint16_t *tlist = nullptr, *slot_of = nullptr;
+    uint32_t *tcnt = nullptr;
     // env tables
     uint32_t *trans = nullptr;
     double *cdf = nullptr;
@@ -648,9 +648,13 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
             return bad(fail(RL_E_HIP, "memset"));
     }
     if (c.agent == RL_AGENT_TRACES) {
-        a->vis_words = (a->S + 31) / 32;
-        if ((rc = dalloc(&a->trace, SA * L)) || (rc = dalloc(&a->visited, (size_t)a->vis_words * L))) return bad(rc);
-        if (hipMemset(a->trace, 0, SA * L * 8) != hipSuccess || hipMemset(a->visited, 0, (size_t)a->vis_words * L * 4) != hipSuccess)
+        if (a->S > 65535) return bad(fail(RL_E_ARG, "traces need S <= 65535"));
+        const size_t SL = (size_t)a->S * L;
+        if ((rc = dalloc(&a->trace, SA * L)) || (rc = dalloc(&a->tlist, SL)) || (rc = dalloc(&a->slot_of, SL)) ||
+            (rc = dalloc(&a->tcnt, L)))
+            return bad(rc);
+        if (hipMemset(a->trace, 0, SA * L * 8) != hipSuccess || hipMemset(a->tlist, 0, SL * 2) != hipSuccess ||
+            hipMemset(a->slot_of, 0, SL * 2) != hipSuccess || hipMemset(a->tcnt, 0, (size_t)L * 4) != hipSuccess)
             return bad(fail(RL_E_HIP, "memset"));
     }
     if (!a->eh.trans.empty() &&
@@ -670,7 +674,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.n_rep = a->n_rep;
     p.delta_words = (uint32_t)a->delta_words;
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
-    p.trace = a->trace; p.visited = a->visited; p.vis_words = a->vis_words;
+    p.trace = a->trace; p.tlist = a->tlist; p.slot_of = a->slot_of; p.tcnt = a->tcnt;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
     p.fixed_start = a->eh.fixed_start;
     p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
@@ -697,7 +701,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->q_base); dfree(a->qf_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own);
     dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
-    dfree(a->trace); dfree(a->visited); dfree(a->trans); dfree(a->cdf);
+    dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d);
     if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
     delete a;
@@ -734,10 +738,7 @@ int rl_agent_reset(rl_agent *a) {
 int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
-    if (a->trace) {
-        HIPC(hipMemsetAsync(a->trace, 0, (size_t)a->S * a->A * a->L * 8, a->stream));
-        HIPC(hipMemsetAsync(a->visited, 0, (size_t)a->vis_words * a->L * 4, a->stream));
-    }
+    if (a->tcnt) HIPC(hipMemsetAsync(a->tcnt, 0, (size_t)a->L * 4, a->stream));   // empty trace sets
     launch_arm_full(a->kp, n_episodes ? RL_MODE_TRAIN : RL_MODE_DONE, 0, 0, 0.0, a->stream);
     HIPC(hipGetLastError());
     if (n_episodes == 0) {
@@ -809,7 +810,7 @@ int rl_agent_stats(rl_agent *a, rl_stats *out) {
     out->reward_sum_q16 = (int64_t)s[4];
     out->done_lanes = s[5];
     out->launches = a->launches;
-    out->reserved = 0;
+    out->trace_states = s[7];
     return RL_OK;
 }
 

@@ -46,10 +46,13 @@ struct KParams {
     double *q_priv;
     uint32_t *n_priv;
     uint64_t *t_priv;      // [L]
-    // eligibility traces (SoA [entry][lane])
-    double *trace;
-    uint32_t *visited;     // [words][L]
-    uint32_t vis_words;
+    // eligibility traces, per lane a sparse set of the episode's visited states:
+    // tlist[j] = j-th visited state, slot_of[s] = its slot (valid iff
+    // slot_of[s] < tcnt && tlist[slot_of[s]] == s), trace[j*A + b] = E[tlist[j]][b]
+    double *trace;         // [S*A][L] (slot-major)
+    uint16_t *tlist;       // [S][L]
+    uint16_t *slot_of;     // [S][L]
+    uint32_t *tcnt;        // [L]
     // env tables
     const uint32_t *trans; // [S][A] packed
     const double *start_cdf;

@@ -86,20 +86,30 @@ void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- replica fold
-// delta += sum over replicas (exact int64), replicas zeroed for the next launch
-__global__ void k_fold_replicas(KParams p) {
-    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= p.delta_words) return;
-    int64_t s = 0;
-    for (uint32_t r = 0; r < p.n_rep; ++r) {
-        int64_t *x = p.delta_rep + (uint64_t)r * p.delta_words + w;
-        s = (int64_t)((uint64_t)s + (uint64_t)*x);
-        *x = 0;
+// delta += sum over replicas (exact int64), replicas zeroed for the next launch.
+// Block = 64 words x 4 replica slices; each thread's replica loads are
+// independent (unrolled) so they are in flight together.
+__global__ void __launch_bounds__(256) k_fold_replicas(KParams p) {
+    __shared__ uint64_t part[4][64];
+    const uint32_t lw = threadIdx.x & 63u, g = threadIdx.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * 64u + lw;
+    uint64_t s = 0;
+    if (w < p.delta_words) {
+        int64_t *x = p.delta_rep + (uint64_t)g * p.delta_words + w;
+        const uint64_t stride = 4ull * p.delta_words;
+        const uint32_t n = p.n_rep > g ? (p.n_rep - g + 3u) / 4u : 0u;
+#pragma unroll 16
+        for (uint32_t i = 0; i < n; ++i) s += (uint64_t)x[i * stride];
+#pragma unroll 16
+        for (uint32_t i = 0; i < n; ++i) x[i * stride] = 0;
     }
-    p.delta[w] = (int64_t)((uint64_t)p.delta[w] + (uint64_t)s);
+    part[g][lw] = s;
+    __syncthreads();
+    if (g == 0 && w < p.delta_words)
+        p.delta[w] = (int64_t)((uint64_t)p.delta[w] + part[0][lw] + part[1][lw] + part[2][lw] + part[3][lw]);
 }
 void launch_fold_replicas(const KParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_fold_replicas, dim3((p.delta_words + 255) / 256), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_fold_replicas, dim3((p.delta_words + 63) / 64), dim3(256), 0, s, p);
 }
 
 // ---------------------------------------------------------------- merge apply

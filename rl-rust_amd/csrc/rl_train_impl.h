@@ -78,6 +78,7 @@ struct LaneRegs {
 struct Counters {
     uint32_t n_train = 0, n_eval = 0, n_tep = 0, n_eep = 0;
     int64_t rsum = 0;      // sum over finished training episodes of rint(reward * 2^16)
+    uint32_t trace_states = 0;   // visited-set entries swept by the eligibility update
 };
 
 __device__ __forceinline__ void lane_load(const KParams &p, uint64_t lane, bool active, LaneRegs &L) {
@@ -114,15 +115,16 @@ __device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, cons
 // Every thread of the block must call these (they contain a barrier).
 __device__ __forceinline__ void flush_block(const KParams &p, unsigned long long *acc) {
     __syncthreads();
-    if (threadIdx.x < 6 && acc[threadIdx.x])
+    if (threadIdx.x < 8 && threadIdx.x != 6 && acc[threadIdx.x])
         atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * 8u + threadIdx.x], acc[threadIdx.x]);
 }
 __device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, const Counters &C,
                                             bool active, unsigned long long *acc) {
-    const uint64_t v[6] = {C.n_train, C.n_eval, C.n_tep, C.n_eep, (uint64_t)C.rsum,
-                           (uint64_t)(active && L.mode == RL_MODE_DONE)};
+    const uint64_t v[8] = {C.n_train, C.n_eval, C.n_tep, C.n_eep, (uint64_t)C.rsum,
+                           (uint64_t)(active && L.mode == RL_MODE_DONE), 0, C.trace_states};
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < 8; ++i) {
+        if (i == 6) continue;
         const int64_t s = wave_sum_i64((int64_t)v[i]);
         if ((threadIdx.x & 63u) == 0 && s != 0) atomicAdd(&acc[i], (unsigned long long)s);
     }
@@ -185,6 +187,57 @@ __device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint6
     p.rec[(uint64_t)k * p.L + lane] = rec;
 }
 
+// E[s][a] += 1 (elegibility_traces_agent.rs:75-80): find s in the lane's sparse
+// set or append it with a fresh zero row (slot-major SoA, coalesced per slot)
+template <int A>
+__device__ __forceinline__ void trace_visit(const KParams &p, uint64_t lane, uint32_t s, uint32_t a,
+                                            uint32_t &cnt) {
+    const uint64_t Ls = p.L;
+    uint32_t j = p.slot_of[(uint64_t)s * Ls + lane];
+    if (j < cnt && p.tlist[(uint64_t)j * Ls + lane] == s) {
+        double *e = &p.trace[((uint64_t)j * A + a) * Ls + lane];
+        *e = *e + 1.0;
+    } else {
+        j = cnt++;
+        p.tlist[(uint64_t)j * Ls + lane] = (uint16_t)s;
+        p.slot_of[(uint64_t)s * Ls + lane] = (uint16_t)j;
+#pragma unroll
+        for (int b = 0; b < A; ++b) p.trace[((uint64_t)j * A + b) * Ls + lane] = (uint32_t)b == a ? 1.0 : 0.0;
+    }
+}
+
+// The eligibility sweep over slots [0, nv): E[o][b] is read, fn(o, b, E) applied,
+// E *= gamma*lambda written back.  TC slots at a time with every load issued
+// before any use (memory-level parallelism; slot j of all lanes is one row).
+template <int A, class Fn>
+__device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uint32_t nv, Fn &&fn) {
+    constexpr uint32_t TC = 4;
+    const uint64_t Ls = p.L;
+    for (uint32_t j0 = 0; j0 < nv; j0 += TC) {
+        uint32_t o[TC];
+        double ev[TC][A];
+#pragma unroll
+        for (uint32_t c = 0; c < TC; ++c) {
+            const bool in = j0 + c < nv;
+            const uint32_t j = in ? j0 + c : j0;
+            o[c] = p.tlist[(uint64_t)j * Ls + lane];
+#pragma unroll
+            for (int b = 0; b < A; ++b) ev[c][b] = p.trace[((uint64_t)j * A + b) * Ls + lane];
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < TC; ++c) {
+            if (j0 + c < nv) {
+                const uint32_t j = j0 + c;
+#pragma unroll
+                for (int b = 0; b < A; ++b) {
+                    fn(o[c], (uint32_t)b, ev[c][b]);
+                    p.trace[((uint64_t)j * A + b) * Ls + lane] = ev[c][b] * p.gl;
+                }
+            }
+        }
+    }
+}
+
 // ======================================================================== shared
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
@@ -239,6 +292,8 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     const bool active = tid < p.G && lane < p.L;
     LaneRegs L;
     lane_load(p, lane, active, L);
+    uint32_t tcnt = 0, trace_states = 0;           // traces: size of the lane's visited set
+    if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
 
     // f64 image of entry idx (exact: |raw| <= 2^52)
     auto val = [&](uint32_t idx, int64_t raw) -> double {
@@ -382,61 +437,21 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             else if (owner) settle(idx);
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
-            // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda.  Per-lane deltas
-            // are summed exactly across the wave; one contribution per wave and entry.
-            const uint64_t Ls = p.L;
-            if (train) {
-                double *e = &p.trace[(uint64_t)(L.s * A + L.a) * Ls + lane];
-                *e = *e + 1.0;
-                p.visited[(uint64_t)(L.s >> 5) * Ls + lane] |= 1u << (L.s & 31u);
-            }
-            for (uint32_t w = 0; w < p.vis_words; ++w) {
-                const uint32_t mine = train ? p.visited[(uint64_t)w * Ls + lane] : 0u;
-                uint32_t uw = wave_or_u32(mine);
-                while (uw) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(uw);
-                    uw &= uw - 1u;
-                    const uint32_t o = w * 32u + bit;
-                    const bool has = (mine >> bit) & 1u;
-#pragma unroll
-                    for (int b = 0; b < A; ++b) {
-                        int64_t d = 0;
-                        uint32_t fl = 0;
-                        if (has) {
-                            double *ep = &p.trace[(uint64_t)(o * A + b) * Ls + lane];
-                            const double ev = *ep;
-                            if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
-                            else d = q_fix_finite(p.lr * (td * ev));
-                            *ep = ev * p.gl;
-                        }
-#pragma unroll
-                        for (int t = 0; t < P; ++t) {
-                            const bool mine_t = has && ut == (uint32_t)t;
-                            const int64_t sum = wave_sum_i64(mine_t ? d : 0);
-                            const uint32_t n = (uint32_t)__popcll(__ballot(mine_t));
-                            uint32_t f = 0;
-                            if constexpr (SPEC) f = wave_or_u32(mine_t ? fl : 0u);
-                            const uint32_t idx = (uint32_t)t * SA + o * A + b;
-                            if ((tid & 63u) == 0 && n) {
-                                if (contribute(idx, sum, n, f) && !sweep)
-                                    LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
-                            }
-                        }
-                    }
-                }
-            }
-            if (train && term) {                          // trace map cleared on termination
-                for (uint32_t w = 0; w < p.vis_words; ++w) {
-                    uint32_t m = p.visited[(uint64_t)w * Ls + lane];
-                    while (m) {
-                        const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-#pragma unroll
-                        for (int b = 0; b < A; ++b) p.trace[(uint64_t)(o * A + b) * Ls + lane] = 0.0;
-                    }
-                    p.visited[(uint64_t)w * Ls + lane] = 0u;
-                }
-            }
+            // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
+            // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
+            // own visited set; slot j of all lanes is one coalesced row.
+            if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
+            const uint32_t nv = train ? tcnt : 0u;
+            trace_states += nv;
+            trace_sweep<A>(p, lane, nv, [&](uint32_t o, uint32_t b, double ev) {
+                uint32_t fl = 0;
+                int64_t d;
+                if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
+                else d = q_fix_finite(p.lr * (td * ev));
+                const uint32_t idx = ut * SA + o * A + b;
+                if (contribute(idx, d, 1u, fl) && !sweep) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
+            });
+            if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
             if (sweep) {
                 if (tid < PSA) settle(tid);
@@ -474,6 +489,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     }
 
     if (active) lane_store(p, lane, L);
+    if constexpr (TRACES) { if (active) p.tcnt[lane] = tcnt; }
     {
         const uint32_t c_done = (uint32_t)__popcll(__ballot(active && L.mode == RL_MODE_DONE));
         if ((tid & 63u) == 0) {
@@ -482,6 +498,10 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             if (c_tep) atomicAdd(&ACC[2], (unsigned long long)c_tep);
             if (c_eep) atomicAdd(&ACC[3], (unsigned long long)c_eep);
             if (c_done) atomicAdd(&ACC[5], (unsigned long long)c_done);
+        }
+        if constexpr (TRACES) {
+            const int64_t ts = wave_sum_i64((int64_t)trace_states);
+            if ((tid & 63u) == 0 && ts) atomicAdd(&ACC[7], (unsigned long long)ts);
         }
         flush_block(p, ACC);
     }
@@ -570,6 +590,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
     const uint32_t SA = p.S * (uint32_t)A;
     const uint64_t Ls = p.L;
     uint64_t t = UCB ? p.t_priv[lane] : 0;
+    uint32_t tcnt = AGENT == RL_AGENT_TRACES ? p.tcnt[lane] : 0u;
 
     auto qref = [&](uint32_t idx) -> double & { return p.q_priv[(uint64_t)idx * Ls + lane]; };
     auto predict = [&](uint32_t s, double (&v)[A]) {
@@ -654,36 +675,13 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
                 double &q = qref(ut * SA + L.s * A + L.a);     // tabular_policy.rs:36
                 q = q + p.lr * td;
             } else {
-                double *e0 = &p.trace[(uint64_t)(L.s * A + L.a) * Ls + lane];
-                *e0 = *e0 + 1.0;
-                p.visited[(uint64_t)(L.s >> 5) * Ls + lane] |= 1u << (L.s & 31u);
-                for (uint32_t w = 0; w < p.vis_words; ++w) {
-                    uint32_t m = p.visited[(uint64_t)w * Ls + lane];
-                    while (m) {
-                        const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-#pragma unroll
-                        for (int b = 0; b < A; ++b) {
-                            double *ep = &p.trace[(uint64_t)(o * A + b) * Ls + lane];
-                            const double ev = *ep;
-                            double &q = qref(ut * SA + o * A + b);
-                            q = q + p.lr * (td * ev);
-                            *ep = ev * p.gl;
-                        }
-                    }
-                }
-                if (term) {
-                    for (uint32_t w = 0; w < p.vis_words; ++w) {
-                        uint32_t m = p.visited[(uint64_t)w * Ls + lane];
-                        while (m) {
-                            const uint32_t o = w * 32u + (uint32_t)__builtin_ctz(m);
-                            m &= m - 1u;
-#pragma unroll
-                            for (int b = 0; b < A; ++b) p.trace[(uint64_t)(o * A + b) * Ls + lane] = 0.0;
-                        }
-                        p.visited[(uint64_t)w * Ls + lane] = 0u;
-                    }
-                }
+                trace_visit<A>(p, lane, L.s, L.a, tcnt);
+                C.trace_states += tcnt;
+                trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) {
+                    double &q = qref(ut * SA + o * A + b);
+                    q = q + p.lr * (td * ev);
+                });
+                if (term) tcnt = 0;
             }
             if (P == 2) L.dflag = !L.dflag;
             if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
@@ -700,6 +698,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
     }
     lane_store(p, lane, L);
     if (UCB) p.t_priv[lane] = t;
+    if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
 }
 
 // ---------------------------------------------------------------- launch table

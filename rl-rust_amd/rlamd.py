@@ -52,7 +52,7 @@ class Stats(C.Structure):
     _fields_ = [("train_steps", C.c_uint64), ("eval_steps", C.c_uint64),
                 ("train_episodes", C.c_uint64), ("eval_episodes", C.c_uint64),
                 ("reward_sum_q16", C.c_int64), ("done_lanes", C.c_uint64),
-                ("launches", C.c_uint64), ("reserved", C.c_uint64)]
+                ("launches", C.c_uint64), ("trace_states", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

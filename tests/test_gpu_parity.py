@@ -168,6 +168,17 @@ def test_private_mode_matches_reference_loop(rl, oracle, case):
     f = oracle.Faithful(dict(p, lane_offset=5))
     f.train(n_ep, n_ep // 6)
     _assert_q_equal(dev.q()[5], f.q())
+    _assert_stats_equal(dev, ref)
+
+
+STAT_KEYS = {0: "train_steps", 1: "eval_steps", 2: "train_episodes", 3: "eval_episodes",
+             4: "reward_sum_q16", 7: "trace_states"}
+
+
+def _assert_stats_equal(dev, ref):
+    d, r = dev.stats(), ref.stats().view(np.int64)
+    for i, k in STAT_KEYS.items():
+        assert d[k] == int(r[i]), (k, d[k], int(r[i]))
 
 
 SHARED_CASES = [
@@ -206,6 +217,7 @@ def test_shared_mode_matches_batched_oracle(rl, oracle, case):
     ref.train_episodes(12, 4)
     _assert_records_equal(dev.records(), ref.records())
     assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
 
 
 def test_full_size_fl8x8_properties(rl):
