@@ -102,7 +102,17 @@ typedef struct rl_step_record {
     double r, td;
 } rl_step_record;
 
-/* Counters accumulated since rl_agent_create / rl_agent_reset_stats. */
+/* One per finished episode (episode log only): the reward_history /
+ * episode_length entries of Agent::train / Agent::evaluate (src/agent.rs:72-141).
+ * seq = the lane's running episode-log index (train and eval episodes interleaved
+ * in the order they finished); mode = RL_MODE_TRAIN or RL_MODE_EVAL. */
+typedef struct rl_episode_record {
+    uint32_t lane, length, seq;
+    uint8_t mode, pad[3];
+    double reward;
+} rl_episode_record;
+
+/* Counters accumulated since rl_agent_create. */
 typedef struct rl_stats {
     uint64_t train_steps;     /* every Env::step inside train, truncation step included */
     uint64_t eval_steps;      /* steps of in-train evaluate() episodes (excluded from the metric) */
@@ -186,6 +196,16 @@ int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n);
 int rl_agent_set_recording(rl_agent *a, int32_t enable);
 int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64_t *n_total);
 int rl_agent_dims(rl_agent *a, uint32_t *n_states, uint32_t *n_actions, uint32_t *n_tables);
+/* episode log (device-side reward_history / episode_length, src/agent.rs:72-141):
+ * a ring of `capacity_per_lane` records per lane ([slot][lane] in HBM); 0 disables.
+ * Enabling (re)allocates and empties the log. */
+int rl_agent_set_episode_log(rl_agent *a, uint32_t capacity_per_lane);
+/* Drain the log: records lane by lane, each lane oldest first.  n_total = records
+ * available (only the first `cap` are written), n_lost = records overwritten
+ * because a lane finished more than capacity_per_lane episodes.  Empties the log
+ * (out == NULL only counts and keeps it). */
+int rl_agent_take_episodes(rl_agent *a, rl_episode_record *out, uint64_t cap, uint64_t *n_total,
+                           uint64_t *n_lost);
 /* raw per-lane records (4 x u32 each): core = {s, flags|a|mode, env word, train episodes},
  * aux = {eps lo, eps hi, eval episodes left, episode length}; for checkpoints and tests */
 int rl_agent_lane_state(rl_agent *a, uint32_t *core, uint32_t *aux, size_t n_lanes);

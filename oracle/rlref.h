@@ -10,7 +10,7 @@
  * (no rustc/cargo in this image), has no tests or fixtures (F2) and
  * draws from an entropy-seeded ChaCha12 ThreadRng (F3), so no reference output
  * can be reproduced.  What IS pinned: hand-derived known-answer tests taken
- * from the reference source (tests/golden/kat.json), and an independent Python
+ * from the reference source (tests/golden/tables.json["kat"]), and an independent Python
  * construction restatement of every transition table (tests/golden/tables.json).
  * The RNG stream (xoshiro128** per lane) replaces ThreadRng at exactly the
  * reference's draw sites, with rand-0.8.5's distribution mappings restated.

@@ -269,6 +269,9 @@ struct rl_agent {
     rl_step_record *rec_d = nullptr;
     bool recording = false;
     std::vector<rl_step_record> rec_h;
+    rl_episode_record *elog_d = nullptr;   // episode log ring [cap][L]
+    uint32_t *elog_cnt_d = nullptr;
+    uint32_t elog_cap = 0;
     uint64_t launches = 0;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -355,6 +358,9 @@ void agent_sync_params(rl_agent *a) {
     p.decay_kind = a->cfg.decay_kind;
     p.algo = a->cfg.algo;
     p.delta = a->delta;
+    p.elog = a->elog_cap ? a->elog_d : nullptr;
+    p.elog_cnt = a->elog_cnt_d;
+    p.elog_cap = a->elog_cap;
 }
 
 int launch_train_kernel(rl_agent *a) {
@@ -702,7 +708,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->trans); dfree(a->cdf);
-    dfree(a->stats_d); dfree(a->rec_d);
+    dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
     delete a;
 }
@@ -938,6 +944,53 @@ int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64
         const size_t n = std::min<size_t>(cap, a->rec_h.size());
         std::memcpy(out, a->rec_h.data(), n * sizeof(rl_step_record));
         a->rec_h.clear();
+    }
+    return RL_OK;
+}
+
+int rl_agent_set_episode_log(rl_agent *a, uint32_t capacity_per_lane) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    HIPC(hipStreamSynchronize(a->stream));
+    dfree(a->elog_d);
+    dfree(a->elog_cnt_d);
+    a->elog_d = nullptr;
+    a->elog_cnt_d = nullptr;
+    a->elog_cap = 0;
+    if (capacity_per_lane) {
+        int rc;
+        if ((rc = dalloc(&a->elog_d, (size_t)capacity_per_lane * a->L)) || (rc = dalloc(&a->elog_cnt_d, a->L)))
+            return rc;
+        HIPC(hipMemset(a->elog_cnt_d, 0, (size_t)a->L * 4));
+        a->elog_cap = capacity_per_lane;
+    }
+    agent_sync_params(a);
+    return RL_OK;
+}
+
+int rl_agent_take_episodes(rl_agent *a, rl_episode_record *out, uint64_t cap, uint64_t *n_total,
+                           uint64_t *n_lost) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (!a->elog_cap) return fail(RL_E_STATE, "episode log not enabled");
+    HIPC(hipSetDevice(a->device));
+    std::vector<uint32_t> cnt(a->L);
+    std::vector<rl_episode_record> ring((size_t)a->elog_cap * a->L);
+    HIPC(hipMemcpyAsync(cnt.data(), a->elog_cnt_d, (size_t)a->L * 4, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipMemcpyAsync(ring.data(), a->elog_d, ring.size() * sizeof(rl_episode_record), hipMemcpyDeviceToHost,
+                        a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    uint64_t total = 0, lost = 0, w = 0;
+    for (uint32_t l = 0; l < a->L; ++l) {
+        const uint32_t c = cnt[l], keep = std::min(c, a->elog_cap);
+        lost += c - keep;
+        for (uint32_t i = c - keep; i < c; ++i, ++total)
+            if (out && w < cap) out[w++] = ring[(size_t)(i % a->elog_cap) * a->L + l];
+    }
+    if (n_total) *n_total = total;
+    if (n_lost) *n_lost = lost;
+    if (out) {   // a NULL `out` only counts (the log is kept)
+        HIPC(hipMemsetAsync(a->elog_cnt_d, 0, (size_t)a->L * 4, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
     }
     return RL_OK;
 }

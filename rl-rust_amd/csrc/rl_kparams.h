@@ -72,6 +72,9 @@ struct KParams {
     // outputs
     unsigned long long *stats; // rl_stats as u64[8] x STATS_REP replicas (block b adds into b % STATS_REP)
     rl_step_record *rec;       // [K][L] or null
+    rl_episode_record *elog;   // episode log [elog_cap][L] or null
+    uint32_t *elog_cnt;        // [L] episodes logged per lane (ring position = cnt % elog_cap)
+    uint32_t elog_cap;
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

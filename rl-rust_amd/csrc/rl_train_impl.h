@@ -170,6 +170,22 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     ev_out = ev;
 }
 
+// episode log: reward_history / episode_length entries (src/agent.rs:96-100,
+// :131-138).  The per-lane count lives in HBM and is touched only at episode
+// end, so the step loop carries no extra register.
+__device__ __forceinline__ void log_episode(const KParams &p, uint64_t lane, const LaneRegs &L, bool train_ep) {
+    const uint32_t c = p.elog_cnt[lane];
+    rl_episode_record e;
+    e.lane = (uint32_t)lane;
+    e.length = L.epi_len;
+    e.seq = c;
+    e.mode = train_ep ? (uint8_t)RL_MODE_TRAIN : (uint8_t)RL_MODE_EVAL;
+    e.pad[0] = e.pad[1] = e.pad[2] = 0;
+    e.reward = L.epi_reward;
+    p.elog[(uint64_t)(c % p.elog_cap) * p.L + lane] = e;
+    p.elog_cnt[lane] = c + 1u;
+}
+
 __device__ __forceinline__ void write_record(const KParams &p, uint32_t k, uint64_t lane, uint32_t kind,
                                              uint32_t s, uint32_t a, uint32_t s2, uint32_t a2, double r,
                                              bool term, double td, uint32_t mode) {
@@ -472,6 +488,7 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
             if (tr) atomicAdd(RSUM, (unsigned long long)(int64_t)__builtin_rint(L.epi_reward * 65536.0));
+            if (p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         } else if (doR) {
             L.s = s2;
             L.a = a2;
@@ -692,6 +709,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
         bool tr, ev;
         after_step(p, L, s2, a2, r, term, tr, ev);
+        if (p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         C.n_tep += tr ? 1u : 0u;
         C.n_eep += ev ? 1u : 0u;
         C.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;

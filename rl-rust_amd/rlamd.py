@@ -62,6 +62,8 @@ RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
                          ("term", "u1"), ("mode", "u1"), ("kind", "u1"), ("pad", "u1", (3,)),
                          ("r", "<f8"), ("td", "<f8")])
 KIND_IDLE, KIND_RESET, KIND_STEP = 0, 1, 2
+EPISODE_DTYPE = np.dtype([("lane", "<u4"), ("length", "<u4"), ("seq", "<u4"), ("mode", "u1"),
+                          ("pad", "u1", (3,)), ("reward", "<f8")])
 
 # every function include/rl.h declares: name -> (restype, argtypes)
 _P = C.POINTER
@@ -96,6 +98,8 @@ SIGNATURES = {
     "rl_agent_get_epsilon": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_set_recording": (C.c_int, [_V, C.c_int32]),
     "rl_agent_take_records": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64)]),
+    "rl_agent_set_episode_log": (C.c_int, [_V, C.c_uint32]),
+    "rl_agent_take_episodes": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64), _P(C.c_uint64)]),
     "rl_agent_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
     "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
     "rl_agent_delta_words": (C.c_int, [_V, _P(C.c_uint64)]),
@@ -330,6 +334,18 @@ class Agent:
         out = np.zeros(n.value, RECORD_DTYPE)
         check(lib().rl_agent_take_records(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out.reshape(-1, self.L)
+
+    def set_episode_log(self, capacity_per_lane):
+        check(lib().rl_agent_set_episode_log(self.h, capacity_per_lane))
+
+    def episodes(self):
+        """Finished episodes since the last call (clears): EPISODE_DTYPE records,
+        lane by lane, each lane oldest first; also returns the overwritten count."""
+        n, lost = C.c_uint64(), C.c_uint64()
+        check(lib().rl_agent_take_episodes(self.h, None, 0, C.byref(n), C.byref(lost)))
+        out = np.zeros(n.value, EPISODE_DTYPE)
+        check(lib().rl_agent_take_episodes(self.h, out.ctypes.data, n.value, C.byref(n), C.byref(lost)))
+        return out, lost.value
 
     def lane_state(self):
         core = np.zeros((self.L, 4), np.uint32)

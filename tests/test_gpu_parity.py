@@ -239,3 +239,51 @@ def test_full_size_fl8x8_properties(rl):
         assert np.isfinite(qq).all() and qq.max() <= 1.0 + 1e-9 and qq.min() >= -1e-9
         a.close()
     assert np.array_equal(qs[0], qs[1])
+
+
+def _episodes_from_records(recs, n_lanes):
+    """reward_history / episode_length per lane from step records
+    (src/agent.rs:83-100: epi_reward += r per step, pushed at termination)."""
+    out = [[] for _ in range(n_lanes)]
+    for lane in range(n_lanes):
+        rew, n = 0.0, 0
+        for rec in recs[:, lane]:
+            if rec["kind"] == 1:
+                rew, n = 0.0, 0
+            elif rec["kind"] == 2:
+                rew += float(rec["r"])
+                n += 1
+                if rec["term"]:
+                    out[lane].append((int(rec["mode"]), n, rew))
+    return out
+
+
+@pytest.mark.parametrize("case", [dict(env="frozen_lake", group_size=1, algo="qlearning"),
+                                  dict(env="taxi", group_size=64, selector="ucb", algo="sarsa"),
+                                  dict(env="blackjack", group_size=32, policy="double", algo="expected_sarsa")],
+                         ids=["fl-private", "taxi-shared-ucb", "bj-shared-double"])
+def test_episode_log_matches_oracle(rl, oracle, case):
+    """Device episode log (reward_history / episode_length of train and the
+    interleaved evaluate) == the episodes in the oracle's step records."""
+    L = 70
+    p = _params(rl, n_lanes=L, sync_every=20, n_episodes_for_decay=40, eval_episodes=5, **case)
+    dev = rl.Agent(p)
+    dev.set_episode_log(64)
+    ref = oracle.Batch(p)
+    ref.set_record(True)
+    dev.train(30, 10)
+    ref.train_episodes(30, 10)
+    eps, lost = dev.episodes()
+    assert lost == 0
+    want = _episodes_from_records(ref.records(), L)
+    got = [[] for _ in range(L)]
+    for e in eps:
+        got[int(e["lane"])].append((int(e["mode"]), int(e["length"]), float(e["reward"])))
+    for lane in range(L):
+        assert len(got[lane]) == len(want[lane]), lane
+        for g, w in zip(got[lane], want[lane]):
+            assert g[0] == w[0] and g[1] == w[1] and np.float64(g[2]).tobytes() == np.float64(w[2]).tobytes()
+    # every lane ran exactly 30 training episodes and 5 eval episodes at each of the
+    # interleave points 0, 10, 20 (episode % eval_at == 0, src/agent.rs:107)
+    assert {sum(1 for g in got[l] if g[0] == 0) for l in range(L)} == {30}
+    assert {sum(1 for g in got[l] if g[0] == 1) for l in range(L)} == {15}
