@@ -1,0 +1,259 @@
+// cli_common.hpp — the shared body of the reference bins
+// (src/bin/{frozen_lake,taxi,cliffwalking,blackjack}.rs): structopt flags with
+// the same names and defaults, the 12-run sweep (one-step / traces x
+// ε-greedy / UCB x sarsa / qlearning / expected_sarsa), `{:.2?}` timing lines,
+// moving averages (src/utils.rs:78-93).  The reference draws plots with
+// plotters; here each figure's series are written as CSV instead.
+//
+// Extensions (not in the reference): --lanes N (default 1: the reference's
+// single env + agent, bit-exact vs the oracle), --group_size G (lanes sharing a
+// Q table; 1 = private agents), --sync_every K, --seed, --device, --out_dir.
+#pragma once
+#include <charconv>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "rl.hpp"
+
+namespace cli {
+
+// ---------------------------------------------------------------- flags
+struct Flag {
+    std::string name, help, value;
+    bool is_bool;
+    char short_name;
+};
+class Flags {
+  public:
+    explicit Flags(std::string prog) : prog_(std::move(prog)) {}
+    void opt(const std::string &name, const std::string &def, const std::string &help, char sh = 0) {
+        flags_[name] = Flag{name, help, def, false, sh};
+        order_.push_back(name);
+    }
+    void flag(const std::string &name, const std::string &help) {
+        flags_[name] = Flag{name, help, "false", true, 0};
+        order_.push_back(name);
+    }
+    void parse(int argc, char **argv) {
+        for (int i = 1; i < argc; ++i) {
+            std::string a = argv[i], v;
+            bool has_v = false;
+            if (a == "-h" || a == "--help") { usage(); std::exit(0); }
+            Flag *f = nullptr;
+            if (a.rfind("--", 0) == 0) {
+                a = a.substr(2);
+                const size_t eq = a.find('=');
+                if (eq != std::string::npos) { v = a.substr(eq + 1); a = a.substr(0, eq); has_v = true; }
+                auto it = flags_.find(a);
+                if (it != flags_.end()) f = &it->second;
+            } else if (a.size() == 2 && a[0] == '-') {
+                for (auto &kv : flags_)
+                    if (kv.second.short_name == a[1]) f = &kv.second;
+            }
+            if (!f) { std::fprintf(stderr, "error: unknown argument '%s'\n", argv[i]); usage(); std::exit(2); }
+            if (f->is_bool) { f->value = "true"; continue; }
+            if (!has_v) {
+                if (i + 1 >= argc) { std::fprintf(stderr, "error: '%s' needs a value\n", argv[i]); std::exit(2); }
+                v = argv[++i];
+            }
+            f->value = v;
+        }
+    }
+    std::string str(const std::string &n) const { return flags_.at(n).value; }
+    double f64(const std::string &n) const { return std::strtod(str(n).c_str(), nullptr); }
+    uint64_t u64(const std::string &n) const { return std::strtoull(str(n).c_str(), nullptr, 0); }
+    bool on(const std::string &n) const { return str(n) == "true"; }
+
+  private:
+    void usage() const {
+        std::printf("%s\n\nUSAGE:\n    %s [FLAGS] [OPTIONS]\n\n", prog_.c_str(), prog_.c_str());
+        for (const auto &n : order_) {
+            const Flag &f = flags_.at(n);
+            std::printf("    %s--%s%s\n            %s%s\n", f.short_name ? (std::string("-") + f.short_name + ", ").c_str() : "",
+                        f.name.c_str(), f.is_bool ? "" : " <value>", f.help.c_str(),
+                        f.is_bool ? "" : (" [default: " + f.value + "]").c_str());
+        }
+    }
+    std::string prog_;
+    std::map<std::string, Flag> flags_;
+    std::vector<std::string> order_;
+};
+
+// the options every bin shares (src/bin/frozen_lake.rs:20-74; BlackJack has no max_steps)
+inline void common_flags(Flags &f, bool max_steps) {
+    f.flag("show_example", "Show example of episode");
+    f.opt("n_episodes", "100000", "Number of episodes for the training", 'n');
+    if (max_steps) f.opt("max_steps", "100", "Maximum number of steps per episode");
+    f.opt("learning_rate", "0.05", "Learning rate of the RL agent");
+    f.opt("initial_epsilon", "1.0", "Initial value for the exploration ratio");
+    f.opt("exploration_time", "0.5", "Value to determine percentage of episodes where exploration is possible;");
+    f.opt("final_epsilon", "0.0", "Final value for the exploration ratio");
+    f.opt("confidence_level", "0.5", "Confidence level for the UCB action selection strategy");
+    f.opt("discount_factor", "0.95", "Discont factor to be used on the temporal difference calculation");
+    f.opt("lambda_factor", "0.5", "Lambda factor to be used on the eligibility traces algorithms");
+    f.opt("moving_average_window", "100", "Moving average window to be used on the visualization of results");
+    // extensions
+    f.opt("lanes", "1", "[rl-rust_amd] env lanes (1 = the reference's single env + agent)");
+    f.opt("group_size", "1", "[rl-rust_amd] lanes sharing one Q table (1 = private reference agents)");
+    f.opt("sync_every", "4096", "[rl-rust_amd] synchronous steps per kernel launch");
+    f.opt("seed", "0x5EED", "[rl-rust_amd] RNG key (replaces thread_rng)");
+    f.opt("device", "0", "[rl-rust_amd] HIP device");
+    f.opt("out_dir", ".", "[rl-rust_amd] where the figure CSVs go (the reference plots PNGs)");
+}
+
+// ---------------------------------------------------------------- formatting
+// Rust's `{}` for f64: shortest round-trip decimal, never exponent notation
+inline std::string rust_f64(double v) {
+    if (std::isnan(v)) return "NaN";
+    if (std::isinf(v)) return v > 0 ? "inf" : "-inf";
+    char buf[512];
+    auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::fixed);
+    return std::string(buf, r.ptr);
+}
+// Rust's `{:.2?}` for std::time::Duration
+inline std::string rust_duration(std::chrono::nanoseconds d) {
+    const double ns = (double)d.count();
+    char buf[64];
+    if (ns >= 1e9) std::snprintf(buf, sizeof buf, "%.2fs", ns / 1e9);
+    else if (ns >= 1e6) std::snprintf(buf, sizeof buf, "%.2fms", ns / 1e6);
+    else if (ns >= 1e3) std::snprintf(buf, sizeof buf, "%.2f\xC2\xB5s", ns / 1e3);
+    else std::snprintf(buf, sizeof buf, "%.2fns", ns);   // fmt_decimal pads the fraction to the precision
+    return buf;
+}
+
+// utils::moving_average (src/utils.rs:78-93): consecutive chunks of `window`
+// values, each summed in order and divided by `window` (the last, shorter
+// chunk too).  window 0 never advances in the reference; here it yields {}.
+inline std::vector<double> moving_average(size_t window, const std::vector<double> &v) {
+    std::vector<double> out;
+    if (window == 0) return out;
+    for (size_t aux = 0; aux < v.size();) {
+        const size_t end = aux + window < v.size() ? aux + window : v.size();
+        double r = 0.0;
+        for (size_t i = aux; i < end; ++i) r += v[i];
+        out.push_back(r / (double)window);
+        aux = end;
+    }
+    return out;
+}
+
+inline void write_csv(const std::string &dir, const std::string &title, const std::vector<std::string> &legends,
+                      const std::vector<std::vector<double>> &series) {
+    const std::string path = dir + "/" + title + ".csv";
+    FILE *f = std::fopen(path.c_str(), "w");
+    if (!f) { std::fprintf(stderr, "cannot write %s\n", path.c_str()); return; }
+    size_t rows = 0;
+    for (size_t j = 0; j < series.size(); ++j) {
+        std::fprintf(f, "%s\"%s\"", j ? "," : "", legends[j].c_str());
+        rows = std::max(rows, series[j].size());
+    }
+    std::fprintf(f, "\n");
+    for (size_t i = 0; i < rows; ++i) {
+        for (size_t j = 0; j < series.size(); ++j)
+            std::fprintf(f, "%s%s", j ? "," : "", i < series[j].size() ? rust_f64(series[j][i]).c_str() : "");
+        std::fprintf(f, "\n");
+    }
+    std::fclose(f);
+}
+
+// ---------------------------------------------------------------- the sweep
+inline const std::vector<std::string> &legends() {
+    static const std::vector<std::string> l = {
+        "ε-Greedy One-Step Sarsa", "ε-Greedy One-Step Qlearning", "ε-Greedy One-Step Expected Sarsa",
+        "UCB One-Step Sarsa",      "UCB One-Step Qlearning",      "UCB One-Step Expected Sarsa",
+        "ε-Greedy Trace Sarsa",    "ε-Greedy Trace Qlearning",    "ε-Greedy Trace Expected Sarsa",
+        "UCB Trace Sarsa",         "UCB Trace Qlearning",         "UCB Trace Expected Sarsa"};
+    return l;
+}
+
+// after-train hook (Blackjack's win-rate loop, src/bin/blackjack.rs:179-207)
+using AfterTrain = std::function<void(rlamd::Agent &, const std::string &legend)>;
+
+// src/bin/frozen_lake.rs:139-216: TabularPolicy(lr, 0.0); ε-greedy with decay
+// `a - ε0/(exploration_time·n)` or UCB(c); one-step and trace agents; every
+// (selector, algo) trains n episodes (eval every n/10), then evaluates n.
+inline int run_sweep(const Flags &f, const rl_env_config &env, const AfterTrain &after = nullptr) {
+    const uint64_t n = f.u64("n_episodes");
+    const size_t maw = (size_t)f.u64("moving_average_window");
+    rl_agent_config c{};
+    c.env = env;
+    c.policy = RL_POLICY_TABULAR;
+    c.decay_kind = RL_DECAY_LINEAR;
+    c.lr = f.f64("learning_rate");
+    c.gamma = f.f64("discount_factor");
+    c.lambda = f.f64("lambda_factor");
+    c.eps0 = f.f64("initial_epsilon");
+    c.eps_decay = c.eps0 / (f.f64("exploration_time") * (double)n);
+    c.eps_final = f.f64("final_epsilon");
+    c.ucb_c = f.f64("confidence_level");
+    c.q_default = 0.0;
+    c.seed = f.u64("seed");
+    c.n_lanes = (uint32_t)f.u64("lanes");
+    c.group_size = (uint32_t)f.u64("group_size");
+    c.sync_every = (uint32_t)f.u64("sync_every");
+    c.eval_episodes = 100;   // src/agent.rs:108
+    c.device = (int32_t)f.u64("device");
+    const bool want_td = c.n_lanes == 1;    // per-step training_error: lane 0 via step records
+    if (!want_td) std::fprintf(stderr, "note: training error curves need --lanes 1\n");
+
+    std::vector<std::vector<double>> tr_r, tr_l, tr_e, te_r, te_l;
+    size_t i = 0;
+    for (int agent_kind : {RL_AGENT_ONE_STEP, RL_AGENT_TRACES}) {
+        rl_agent_config ac = c;
+        ac.agent = agent_kind;
+        ac.selector = RL_SEL_EPS_GREEDY;
+        ac.algo = RL_ALGO_SARSA;
+        rlamd::Agent agent(ac);
+        for (int sel : {RL_SEL_EPS_GREEDY, RL_SEL_UCB}) {
+            agent.set_action_selector(sel);
+            for (int algo : {RL_ALGO_SARSA, RL_ALGO_QLEARNING, RL_ALGO_EXPECTED_SARSA}) {
+                agent.set_future_q_value_func(algo);
+                const auto t0 = std::chrono::steady_clock::now();
+                rlamd::Histories h = agent.train(n, n / 10, want_td);
+                const auto el = std::chrono::steady_clock::now() - t0;
+                std::printf("%s %s\n", legends()[i].c_str(),
+                            rust_duration(std::chrono::duration_cast<std::chrono::nanoseconds>(el)).c_str());
+                std::fflush(stdout);
+                tr_e.push_back(moving_average(maw ? h.training_error.size() / maw : 0, h.training_error));
+                tr_r.push_back(moving_average(maw ? n / maw : 0, h.reward));
+                tr_l.push_back(moving_average(maw ? n / maw : 0, h.length));
+                if (f.on("show_example")) {            // Agent::example (src/agent.rs:143-163)
+                    rlamd::Histories ex = agent.evaluate(1);
+                    std::printf("episode reward %s\nterminated with %s steps\n", rust_f64(ex.reward[0]).c_str(),
+                                rust_f64(ex.length[0]).c_str());
+                }
+                if (after) after(agent, legends()[i]);
+                rlamd::Histories e = agent.evaluate(n);
+                te_r.push_back(moving_average(maw ? n / maw : 0, e.reward));
+                te_l.push_back(moving_average(maw ? n / maw : 0, e.length));
+                ++i;
+                agent.reset();
+            }
+        }
+    }
+    const std::string dir = f.str("out_dir");
+    write_csv(dir, "Train Rewards", legends(), tr_r);
+    write_csv(dir, "Train Episodes Length", legends(), tr_l);
+    write_csv(dir, "Training Error", legends(), tr_e);
+    write_csv(dir, "Test Rewards", legends(), te_r);
+    write_csv(dir, "Test Episodes Length", legends(), te_l);
+    return 0;
+}
+
+inline int guarded(const std::function<int()> &fn) {
+    try {
+        return fn();
+    } catch (const rlamd::Error &e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+}
+
+}  // namespace cli
