@@ -196,6 +196,11 @@ int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n);
 int rl_agent_set_recording(rl_agent *a, int32_t enable);
 int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64_t *n_total);
 int rl_agent_dims(rl_agent *a, uint32_t *n_states, uint32_t *n_actions, uint32_t *n_tables);
+/* InternalModelAgent::new(agent, RandomModel::default(), planning_steps)
+ * (src/agent/internal_model_agent.rs:20-31, src/model/random_model.rs): Dyna
+ * planning after every training update; 0 = the plain agent.  Private mode
+ * (group_size 1) only; the model is emptied here and by rl_agent_reset. */
+int rl_agent_set_planning(rl_agent *a, uint32_t planning_steps);
 /* episode log (device-side reward_history / episode_length, src/agent.rs:72-141):
  * a ring of `capacity_per_lane` records per lane ([slot][lane] in HBM); 0 disables.
  * Enabling (re)allocates and empties the log. */

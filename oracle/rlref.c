@@ -162,6 +162,44 @@ static uint32_t uniform_action(rlo_rng *r, uint32_t A) {
         if (!rej) return a;
     }
 }
+/* rand 0.8.5 Rng::gen_range(0..range) for usize = UniformInt::sample_single_inclusive
+ * (RandomModel::get_info, src/model/random_model.rs:29-31): the "conservative but
+ * fast" zone (range << leading_zeros(range)) - 1, widening multiply, reject lo > zone. */
+uint64_t rlo_gen_index_u64(uint64_t v, uint64_t range, int *reject) {
+    const uint64_t zone = (range << __builtin_clzll(range)) - 1u;
+    unsigned __int128 m = (unsigned __int128)v * range;
+    *reject = !((uint64_t)m <= zone);
+    return (uint64_t)(m >> 64);
+}
+static uint32_t gen_index(rlo_rng *r, uint32_t n) {
+    for (;;) {
+        int rej;
+        uint64_t i = rlo_gen_index_u64(next_u64(r), n, &rej);
+        if (!rej) return (uint32_t)i;
+    }
+}
+
+/* RandomModel (src/model/random_model.rs): IndexMap<(s,a),(s',r)> in insertion
+ * order; add_info keeps the FIRST transition seen for (s,a) (entry().or_insert).
+ * Stored as a sparse set: slot[k] is valid iff slot[k] < cnt && key[slot[k]] == k. */
+typedef struct {
+    uint32_t cnt;
+    uint32_t *key, *s2, *slot;
+    double *r;
+} model_t;
+static void model_alloc(model_t *m, size_t nsa) {
+    m->cnt = 0;
+    m->key = (uint32_t *)calloc(nsa, 4); m->s2 = (uint32_t *)calloc(nsa, 4);
+    m->slot = (uint32_t *)calloc(nsa, 4); m->r = (double *)calloc(nsa, 8);
+}
+static void model_free(model_t *m) { free(m->key); free(m->s2); free(m->slot); free(m->r); memset(m, 0, sizeof *m); }
+static void model_add(model_t *m, uint32_t k, uint32_t s2, double r) {
+    uint32_t j = m->slot[k];
+    if (j < m->cnt && m->key[j] == k) return;
+    j = m->cnt++;
+    m->key[j] = k; m->s2[j] = s2; m->r[j] = r; m->slot[k] = j;
+}
+
 /* rand 0.8.5 UniformInt<u8> (u32 large type) for Uniform::from(1..11)
  * (blackjack.rs:542,562): range 10, ints_to_reject = (2^32-10)%10 = 6. */
 uint32_t rlo_uniform_card_u32(uint32_t v, int *reject) {
@@ -553,6 +591,8 @@ struct rlo_faithful {
     uint8_t *visited;    /* [S] — membership of the trace FxHashMap */
     vec reward_history, episode_length, training_error, records;
     int record;
+    uint32_t plan;       /* InternalModelAgent planning steps (0: plain agent) */
+    model_t model;
 };
 
 static void f_clear_policy(rlo_faithful *f) {
@@ -588,6 +628,7 @@ void rlo_faithful_destroy(rlo_faithful *f) {
     if (!f) return;
     free(f->q); free(f->ucb_n); free(f->trace); free(f->visited);
     free(f->reward_history.p); free(f->episode_length.p); free(f->training_error.p); free(f->records.p);
+    model_free(&f->model);
     free(f);
 }
 void rlo_faithful_set_record(rlo_faithful *f, int e) { f->record = e; }
@@ -663,6 +704,29 @@ static double f_update(rlo_faithful *f, uint32_t s, uint32_t a, double r, int te
     return td;
 }
 
+/* InternalModelAgent::update (src/agent/internal_model_agent.rs:47-77): the inner
+ * update, then model.add_info, then planning_steps replays of a uniformly drawn
+ * model entry through the inner get_action + update(terminated = false). */
+static double f_agent_update(rlo_faithful *f, uint32_t s, uint32_t a, double r, int term, uint32_t s2,
+                             uint32_t a2) {
+    double td = f_update(f, s, a, r, term, s2, a2);
+    if (!f->plan) return td;
+    model_add(&f->model, s * f->A + a, s2, r);
+    for (uint32_t i = 0; i < f->plan; ++i) {
+        uint32_t j = gen_index(&f->rng, f->model.cnt);
+        uint32_t k = f->model.key[j], ps = k / f->A, pa = k % f->A, ps2 = f->model.s2[j];
+        double pr = f->model.r[j];
+        uint32_t na = f_get_action(f, ps2);
+        f_update(f, ps, pa, pr, 0, ps2, na);
+    }
+    return td;
+}
+void rlo_faithful_set_planning(rlo_faithful *f, uint32_t planning_steps) {
+    model_free(&f->model);
+    f->plan = planning_steps;
+    if (planning_steps) model_alloc(&f->model, (size_t)f->S * f->A);
+}
+
 /* Agent::evaluate: src/agent.rs:120-141 */
 uint64_t rlo_faithful_evaluate(rlo_faithful *f, uint64_t n_episodes) {
     uint64_t steps = 0;
@@ -693,7 +757,7 @@ uint64_t rlo_faithful_train(rlo_faithful *f, uint64_t n_episodes, uint64_t eval_
             uint32_t s2; double r; int term;
             if (env_step(&f->E, &f->st, a, &f->rng, &s2, &r, &term)) abort();
             uint32_t a2 = f_get_action(f, s2);
-            double td = f_update(f, s, a, r, term, s2, a2);
+            double td = f_agent_update(f, s, a, r, term, s2, a2);
             vpush(&f->training_error, &td);
             if (f->record) {
                 rlo_record rec;
@@ -713,7 +777,7 @@ uint64_t rlo_faithful_train(rlo_faithful *f, uint64_t n_episodes, uint64_t eval_
     return steps;
 }
 /* Agent::reset (one_step_agent.rs:43-46): selector.reset + policy.reset (flag kept) */
-void rlo_faithful_reset(rlo_faithful *f) { f_reset_selector(f); f_clear_policy(f); }
+void rlo_faithful_reset(rlo_faithful *f) { f_reset_selector(f); f_clear_policy(f); f->model.cnt = 0; }
 void rlo_faithful_get_q(const rlo_faithful *f, double *out) {
     memcpy(out, f->q, sizeof(double) * f->P * f->S * f->A);
 }
@@ -764,6 +828,7 @@ typedef struct {
     double *qd;          /* [P][S][A] f64 */
     uint32_t *n;         /* [S][A] */
     uint64_t t;
+    model_t model;       /* InternalModelAgent's RandomModel (private mode) */
 } lane_t;
 
 struct rlo_batch {
@@ -791,6 +856,7 @@ struct rlo_batch {
     int record;
     vec records;
     uint64_t stats[8];
+    uint32_t plan;       /* Dyna planning steps per update (private mode only) */
 };
 
 /* Fixed-point Q (shared mode).  |Q raw| <= 2^52, so every entry converts to
@@ -905,6 +971,7 @@ void rlo_batch_destroy(rlo_batch *b) {
     if (!b) return;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
         free(b->lanes[i].trace); free(b->lanes[i].visited); free(b->lanes[i].qd); free(b->lanes[i].n);
+        model_free(&b->lanes[i].model);
     }
     free(b->lanes); free(b->q_base); free(b->f_base); free(b->q_g); free(b->f_g); free(b->dq);
     free(b->df); free(b->dc); free(b->acc_c); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
@@ -929,7 +996,17 @@ void rlo_batch_reset(rlo_batch *b) {
             memset(L->n, 0, sizeof(uint32_t) * b->S * b->A);
             L->t = 1;
         }
+        L->model.cnt = 0;                    /* model.reset (internal_model_agent.rs:79-82) */
     }
+}
+int rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps) {
+    if (planning_steps && !b->priv) return -1;   /* Dyna: private agents only */
+    b->plan = planning_steps;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+        model_free(&b->lanes[i].model);
+        if (planning_steps) model_alloc(&b->lanes[i].model, (size_t)b->S * b->A);
+    }
+    return 0;
 }
 void rlo_batch_set_selector(rlo_batch *b, int32_t sel) {
     b->c.selector = sel;
@@ -970,6 +1047,52 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
 static int64_t mean_delta(int64_t sum, int64_t n) {
     if (n <= 0) return 0;
     return (int64_t)trunc((double)sum * (1.0 / (double)n));
+}
+
+/* Agent::update of one lane against the current Q / UCB state
+ * (one_step_agent.rs:53-86, elegibility_traces_agent.rs:61-104), with
+ * after_update and the termination hooks */
+static double b_update(rlo_batch *b, lane_t *L, uint32_t s, uint32_t a, double r, int term, uint32_t s2,
+                       uint32_t a2) {
+    const uint32_t A = b->A;
+    const int ucb = b->c.selector == RLO_SEL_UCB;
+    uint32_t vt = (b->P == 2 && !L->dflag) ? 1 : 0;   /* get_values table */
+    uint32_t ut = (b->P == 2 && L->dflag) ? 1 : 0;    /* update table */
+    double q2[MAXA], p[MAXA], q[MAXA];
+    b_row(b, vt, s2, q2);
+    if (!ucb) eps_probs(L->eps, q2, A, p);
+    else if (b->c.algo == RLO_ALGO_EXPECTED_SARSA) {
+        uint64_t n64[MAXA];
+        for (uint32_t i = 0; i < A; ++i) n64[i] = b->n_g[(size_t)s2 * A + i];
+        ucb_probs(q2, n64, b->t_g, b->c.ucb_c, A, p);
+    }
+    double fq = future_q(b->c.algo, q2, a2, p, A);
+    b_row(b, vt, s, q);
+    double td = r + b->c.gamma * fq - q[a];
+    if (b->c.agent == RLO_AGENT_ONE_STEP) {
+        add_delta(b, ut, s, a, b->c.lr * td);
+    } else {
+        L->trace[(size_t)s * A + a] += 1.0;
+        L->visited[s] = 1;
+        for (uint32_t o = 0; o < b->S; ++o) {
+            if (!L->visited[o]) continue;
+            b->stats[7]++;                    /* visited-set entries swept (V per step) */
+            for (uint32_t bb = 0; bb < A; ++bb) {
+                double *e = &L->trace[(size_t)o * A + bb];
+                add_delta(b, ut, o, bb, b->c.lr * (td * *e));
+                *e *= b->c.gamma * b->c.lambda_;
+            }
+        }
+    }
+    if (b->P == 2) L->dflag = !L->dflag;
+    if (term) {
+        if (b->c.agent == RLO_AGENT_TRACES) {
+            memset(L->trace, 0, sizeof(double) * b->S * A);
+            memset(L->visited, 0, b->S);
+        }
+        if (!ucb) L->eps = decay_eps(&b->c, L->eps);
+    }
+    return td;
 }
 
 /* One synchronous step of a learner group.  Every live lane does exactly one
@@ -1028,41 +1151,17 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
         int term = tv[j];
         double td = 0.0;
         if (L->mode == RLO_MODE_TRAIN) {
-            uint32_t vt = (b->P == 2 && !L->dflag) ? 1 : 0;   /* get_values table */
-            uint32_t ut = (b->P == 2 && L->dflag) ? 1 : 0;    /* update table */
-            double q2[MAXA], p[MAXA], q[MAXA];
-            b_row(b, vt, s2, q2);
-            if (!ucb) eps_probs(L->eps, q2, A, p);
-            else if (b->c.algo == RLO_ALGO_EXPECTED_SARSA) {
-                uint64_t n64[MAXA];
-                for (uint32_t i = 0; i < A; ++i) n64[i] = b->n_g[(size_t)s2 * A + i];
-                ucb_probs(q2, n64, b->t_g, b->c.ucb_c, A, p);
-            }
-            double fq = future_q(b->c.algo, q2, a2, p, A);
-            b_row(b, vt, s, q);
-            td = r + b->c.gamma * fq - q[a];
-            if (b->c.agent == RLO_AGENT_ONE_STEP) {
-                add_delta(b, ut, s, a, b->c.lr * td);
-            } else {
-                L->trace[(size_t)s * A + a] += 1.0;
-                L->visited[s] = 1;
-                for (uint32_t o = 0; o < b->S; ++o) {
-                    if (!L->visited[o]) continue;
-                    b->stats[7]++;                    /* visited-set entries swept (V per step) */
-                    for (uint32_t bb = 0; bb < A; ++bb) {
-                        double *e = &L->trace[(size_t)o * A + bb];
-                        add_delta(b, ut, o, bb, b->c.lr * (td * *e));
-                        *e *= b->c.gamma * b->c.lambda_;
-                    }
+            td = b_update(b, L, s, a, r, term, s2, a2);
+            if (b->plan) {                        /* InternalModelAgent (private mode) */
+                model_add(&L->model, s * A + a, s2, r);
+                for (uint32_t i = 0; i < b->plan; ++i) {
+                    uint32_t jj = gen_index(&L->rng, L->model.cnt);
+                    uint32_t k = L->model.key[jj], ps = k / A, pa = k % A, ps2 = L->model.s2[jj];
+                    double pr = L->model.r[jj];
+                    uint32_t na = b_select(b, L, ps2);
+                    if (ucb) { b->n_g[(size_t)ps2 * A + na] += 1; b->t_g += 1; }
+                    b_update(b, L, ps, pa, pr, 0, ps2, na);
                 }
-            }
-            if (b->P == 2) L->dflag = !L->dflag;
-            if (term) {
-                if (b->c.agent == RLO_AGENT_TRACES) {
-                    memset(L->trace, 0, sizeof(double) * b->S * A);
-                    memset(L->visited, 0, b->S);
-                }
-                if (!ucb) L->eps = decay_eps(&b->c, L->eps);
             }
             b->stats[0]++;
         } else {

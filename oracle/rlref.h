@@ -87,6 +87,9 @@ int      rlo_env_start(const rlo_config *c, double *start);   /* initial-state d
 int      rlo_env_walk(const rlo_config *c, uint64_t lane, uint32_t n, const uint32_t *actions,
                       uint32_t *s0, uint32_t *s_next, double *reward, uint8_t *term);
 
+/* rand 0.8.5 gen_range(0..range) for usize (sample_single_inclusive): index + reject flag */
+uint64_t rlo_gen_index_u64(uint64_t v, uint64_t range, int *reject);
+
 /* ---------------- faithful single-env restatement (f64) ---------------- */
 typedef struct rlo_faithful rlo_faithful;
 rlo_faithful *rlo_faithful_create(const rlo_config *c);
@@ -105,6 +108,9 @@ void   rlo_faithful_histories(const rlo_faithful *f, double *reward_history,
 uint64_t rlo_faithful_get_records(const rlo_faithful *f, rlo_record *out, uint64_t cap);
 void   rlo_faithful_set_record(rlo_faithful *f, int enable);
 double rlo_faithful_epsilon(const rlo_faithful *f);
+/* InternalModelAgent::new(agent, RandomModel::default(), planning_steps)
+ * (src/agent/internal_model_agent.rs:20-31); 0 = the plain agent */
+void   rlo_faithful_set_planning(rlo_faithful *f, uint32_t planning_steps);
 /* the bench cpu baseline: train for `budget_steps` env steps and return the
  * steps actually run (whole episodes), no recording */
 uint64_t rlo_faithful_bench(const rlo_config *c, uint64_t n_episodes, uint64_t eval_at,
@@ -139,6 +145,8 @@ void   rlo_batch_stats(const rlo_batch *b, uint64_t *out8);
 void   rlo_batch_lane_eps(const rlo_batch *b, double *out);
 void   rlo_batch_set_selector(rlo_batch *b, int32_t selector);
 void   rlo_batch_set_algo(rlo_batch *b, int32_t algo);
+/* Dyna planning steps per update (private mode only; -1 otherwise) */
+int    rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps);
 
 #ifdef __cplusplus
 }

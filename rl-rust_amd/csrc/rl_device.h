@@ -70,6 +70,16 @@ __device__ __forceinline__ uint32_t uniform_action(Rng &r) {
         if (lo <= zone) return (uint32_t)hi;
     }
 }
+// rand 0.8.5 Rng::gen_range(0..n) for usize = sample_single_inclusive: the
+// "conservative" zone (n << lz(n)) - 1 (RandomModel::get_info, random_model.rs:29-31)
+__device__ __forceinline__ uint32_t gen_index(Rng &r, uint32_t n) {
+    const uint64_t range = n;
+    const uint64_t zone = (range << __clzll((long long)range)) - 1ull;
+    for (;;) {
+        const uint64_t v = r.next_u64();
+        if (v * range <= zone) return (uint32_t)__umul64hi(v, range);
+    }
+}
 // rand 0.8.5 UniformInt<u8>(1..11) with u32 large type (blackjack.rs:542,562)
 __device__ __forceinline__ uint32_t draw_card(Rng &r) {
     constexpr uint32_t zone = 0xFFFFFFFFu - 6u;

@@ -261,6 +261,10 @@ struct rl_agent {
     double *trace = nullptr;
     uint16_t *tlist = nullptr, *slot_of = nullptr;
     uint32_t *tcnt = nullptr;
+    // Dyna model (private mode)
+    uint32_t plan = 0;
+    uint32_t *mcnt = nullptr, *mkey = nullptr, *ms2 = nullptr, *mslot = nullptr;
+    double *mr = nullptr;
     // env tables
     uint32_t *trans = nullptr;
     double *cdf = nullptr;
@@ -358,6 +362,8 @@ void agent_sync_params(rl_agent *a) {
     p.decay_kind = a->cfg.decay_kind;
     p.algo = a->cfg.algo;
     p.delta = a->delta;
+    p.plan_steps = a->plan;
+    p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;
     p.elog = a->elog_cap ? a->elog_d : nullptr;
     p.elog_cnt = a->elog_cnt_d;
     p.elog_cap = a->elog_cap;
@@ -709,6 +715,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
+    dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
     if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
     delete a;
 }
@@ -736,6 +743,7 @@ int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double e
 int rl_agent_reset(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
+    if (a->mcnt) HIPC(hipMemsetAsync(a->mcnt, 0, (size_t)a->L * 4, a->stream));   // model.reset
     int rc = agent_reset_policy(a);
     if (rc) return rc;
     return agent_reset_selector(a);
@@ -945,6 +953,29 @@ int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64
         std::memcpy(out, a->rec_h.data(), n * sizeof(rl_step_record));
         a->rec_h.clear();
     }
+    return RL_OK;
+}
+
+int rl_agent_set_planning(rl_agent *a, uint32_t planning_steps) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (planning_steps && !a->priv) return fail(RL_E_ARG, "Dyna planning needs group_size 1 (private agents)");
+    HIPC(hipSetDevice(a->device));
+    HIPC(hipStreamSynchronize(a->stream));
+    dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
+    a->mcnt = a->mkey = a->ms2 = a->mslot = nullptr;
+    a->mr = nullptr;
+    a->plan = 0;
+    if (planning_steps) {
+        const size_t n = (size_t)a->S * a->A * a->L;
+        int rc;
+        if ((rc = dalloc(&a->mcnt, a->L)) || (rc = dalloc(&a->mkey, n)) || (rc = dalloc(&a->ms2, n)) ||
+            (rc = dalloc(&a->mslot, n)) || (rc = dalloc(&a->mr, n)))
+            return rc;
+        HIPC(hipMemset(a->mcnt, 0, (size_t)a->L * 4));
+        HIPC(hipMemset(a->mslot, 0, n * 4));
+        a->plan = planning_steps;
+    }
+    agent_sync_params(a);
     return RL_OK;
 }
 

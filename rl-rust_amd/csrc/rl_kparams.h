@@ -53,6 +53,12 @@ struct KParams {
     uint16_t *tlist;       // [S][L]
     uint16_t *slot_of;     // [S][L]
     uint32_t *tcnt;        // [L]
+    // Dyna (InternalModelAgent + RandomModel, private mode): per-lane model as a
+    // sparse set in insertion order, entry j = (key = s*A+a, s', r)
+    uint32_t plan_steps;
+    uint32_t *mcnt;        // [L]
+    uint32_t *mkey, *ms2, *mslot;   // [S*A][L]
+    double *mr;            // [S*A][L]
     // env tables
     const uint32_t *trans; // [S][A] packed
     const double *start_cdf;

@@ -636,6 +636,48 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             return a;
         }
     };
+    // Agent::update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
+    // against the lane's current Q, with after_update and the termination hooks
+    auto update = [&](uint32_t s, uint32_t a, double r, bool term, uint32_t s2, uint32_t a2) -> double {
+        const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;
+        const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;
+        double q2[A], pr[A];
+#pragma unroll
+        for (int i = 0; i < A; ++i) { q2[i] = qref(vt * SA + s2 * A + i); pr[i] = 0.0; }
+        if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) {
+            if constexpr (!UCB) {
+                eps_probs<A>(L.eps, q2, pr);
+            } else {
+                const double lnt = rl_log((double)t);
+                double sum = 0.0;
+#pragma unroll
+                for (int i = 0; i < A; ++i) {
+                    pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)p.n_priv[(uint64_t)(s2 * A + i) * Ls + lane]);
+                    sum += pr[i];
+                }
+#pragma unroll
+                for (int i = 0; i < A; ++i) pr[i] /= sum;
+            }
+        }
+        const double fq = future_q<ALGO, A>(q2, a2, pr);
+        const double qa = qref(vt * SA + s * A + a);
+        const double td = r + p.gamma * fq - qa;
+        if constexpr (AGENT == RL_AGENT_ONE_STEP) {
+            double &q = qref(ut * SA + s * A + a);             // tabular_policy.rs:36
+            q = q + p.lr * td;
+        } else {
+            trace_visit<A>(p, lane, s, a, tcnt);
+            C.trace_states += tcnt;
+            trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) {
+                double &q = qref(ut * SA + o * A + b);
+                q = q + p.lr * (td * ev);
+            });
+            if (term) tcnt = 0;
+        }
+        if (P == 2) L.dflag = !L.dflag;                        // after_update
+        if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
+        return td;
+    };
 
     for (uint32_t k = 0; k < p.K; ++k) {
         if (L.mode == RL_MODE_DONE) {
@@ -664,44 +706,32 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         const uint32_t a2 = select(s2);
         double td = 0.0;
         if (L.mode == RL_MODE_TRAIN) {
-            const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;
-            const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;
-            double q2[A], pr[A];
-#pragma unroll
-            for (int i = 0; i < A; ++i) { q2[i] = qref(vt * SA + s2 * A + i); pr[i] = 0.0; }
-            if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) {
-                if constexpr (!UCB) {
-                    eps_probs<A>(L.eps, q2, pr);
-                } else {
-                    const double lnt = rl_log((double)t);
-                    double sum = 0.0;
-#pragma unroll
-                    for (int i = 0; i < A; ++i) {
-                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt,
-                                          (double)p.n_priv[(uint64_t)(s2 * A + i) * Ls + lane]);
-                        sum += pr[i];
-                    }
-#pragma unroll
-                    for (int i = 0; i < A; ++i) pr[i] /= sum;
+            td = update(L.s, L.a, r, term, s2, a2);
+            if (p.plan_steps) {
+                // InternalModelAgent (src/agent/internal_model_agent.rs:47-77): model.add_info
+                // keeps the first (s', r) seen for (s, a) (random_model.rs:34-38), then
+                // planning_steps replays of a uniformly drawn entry (gen_range, :29-31)
+                // through get_action + update(terminated = false)
+                uint32_t mc = p.mcnt[lane];
+                const uint32_t key = L.s * A + L.a;
+                const uint32_t j0 = p.mslot[(uint64_t)key * Ls + lane];
+                if (!(j0 < mc && p.mkey[(uint64_t)j0 * Ls + lane] == key)) {
+                    p.mkey[(uint64_t)mc * Ls + lane] = key;
+                    p.ms2[(uint64_t)mc * Ls + lane] = s2;
+                    p.mr[(uint64_t)mc * Ls + lane] = r;
+                    p.mslot[(uint64_t)key * Ls + lane] = mc;
+                    ++mc;
+                    p.mcnt[lane] = mc;
+                }
+                for (uint32_t i = 0; i < p.plan_steps; ++i) {
+                    const uint32_t j = gen_index(L.rng, mc);
+                    const uint32_t pk = p.mkey[(uint64_t)j * Ls + lane];
+                    const uint32_t ps2 = p.ms2[(uint64_t)j * Ls + lane];
+                    const double pr = p.mr[(uint64_t)j * Ls + lane];
+                    const uint32_t na = select(ps2);
+                    update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
                 }
             }
-            const double fq = future_q<ALGO, A>(q2, a2, pr);
-            const double qa = qref(vt * SA + L.s * A + L.a);
-            td = r + p.gamma * fq - qa;
-            if constexpr (AGENT == RL_AGENT_ONE_STEP) {
-                double &q = qref(ut * SA + L.s * A + L.a);     // tabular_policy.rs:36
-                q = q + p.lr * td;
-            } else {
-                trace_visit<A>(p, lane, L.s, L.a, tcnt);
-                C.trace_states += tcnt;
-                trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) {
-                    double &q = qref(ut * SA + o * A + b);
-                    q = q + p.lr * (td * ev);
-                });
-                if (term) tcnt = 0;
-            }
-            if (P == 2) L.dflag = !L.dflag;
-            if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
             C.n_train++;
         } else {
             C.n_eval++;

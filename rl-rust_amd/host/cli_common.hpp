@@ -176,10 +176,24 @@ inline const std::vector<std::string> &legends() {
 // after-train hook (Blackjack's win-rate loop, src/bin/blackjack.rs:179-207)
 using AfterTrain = std::function<void(rlamd::Agent &, const std::string &legend)>;
 
+// One agent object of a bin and the runs it makes (the reference reuses each
+// agent across runs: set_action_selector, set_future_q_value_func, train,
+// evaluate, reset).  planning > 0 wraps it in InternalModelAgent + RandomModel.
+struct RunSpec {
+    std::string legend;
+    int selector, algo;
+};
+struct AgentSpec {
+    int agent;
+    uint32_t planning;
+    std::vector<RunSpec> runs;
+};
+
 // src/bin/frozen_lake.rs:139-216: TabularPolicy(lr, 0.0); ε-greedy with decay
-// `a - ε0/(exploration_time·n)` or UCB(c); one-step and trace agents; every
-// (selector, algo) trains n episodes (eval every n/10), then evaluates n.
-inline int run_sweep(const Flags &f, const rl_env_config &env, const AfterTrain &after = nullptr) {
+// `a - ε0/(exploration_time·n)` or UCB(c); each run trains n episodes (eval
+// every n/10), prints `{legend} {elapsed:.2?}`, then evaluates n episodes.
+inline int run_agents(const Flags &f, const rl_env_config &env, const std::vector<AgentSpec> &specs,
+                      const AfterTrain &after = nullptr) {
     const uint64_t n = f.u64("n_episodes");
     const size_t maw = (size_t)f.u64("moving_average_window");
     rl_agent_config c{};
@@ -203,48 +217,61 @@ inline int run_sweep(const Flags &f, const rl_env_config &env, const AfterTrain 
     const bool want_td = c.n_lanes == 1;    // per-step training_error: lane 0 via step records
     if (!want_td) std::fprintf(stderr, "note: training error curves need --lanes 1\n");
 
+    std::vector<std::string> legend;
     std::vector<std::vector<double>> tr_r, tr_l, tr_e, te_r, te_l;
-    size_t i = 0;
-    for (int agent_kind : {RL_AGENT_ONE_STEP, RL_AGENT_TRACES}) {
+    for (const AgentSpec &spec : specs) {
         rl_agent_config ac = c;
-        ac.agent = agent_kind;
-        ac.selector = RL_SEL_EPS_GREEDY;
-        ac.algo = RL_ALGO_SARSA;
+        ac.agent = spec.agent;
+        ac.selector = spec.runs.empty() ? RL_SEL_EPS_GREEDY : spec.runs[0].selector;
+        ac.algo = spec.runs.empty() ? RL_ALGO_SARSA : spec.runs[0].algo;
         rlamd::Agent agent(ac);
-        for (int sel : {RL_SEL_EPS_GREEDY, RL_SEL_UCB}) {
-            agent.set_action_selector(sel);
-            for (int algo : {RL_ALGO_SARSA, RL_ALGO_QLEARNING, RL_ALGO_EXPECTED_SARSA}) {
-                agent.set_future_q_value_func(algo);
-                const auto t0 = std::chrono::steady_clock::now();
-                rlamd::Histories h = agent.train(n, n / 10, want_td);
-                const auto el = std::chrono::steady_clock::now() - t0;
-                std::printf("%s %s\n", legends()[i].c_str(),
-                            rust_duration(std::chrono::duration_cast<std::chrono::nanoseconds>(el)).c_str());
-                std::fflush(stdout);
-                tr_e.push_back(moving_average(maw ? h.training_error.size() / maw : 0, h.training_error));
-                tr_r.push_back(moving_average(maw ? n / maw : 0, h.reward));
-                tr_l.push_back(moving_average(maw ? n / maw : 0, h.length));
-                if (f.on("show_example")) {            // Agent::example (src/agent.rs:143-163)
-                    rlamd::Histories ex = agent.evaluate(1);
-                    std::printf("episode reward %s\nterminated with %s steps\n", rust_f64(ex.reward[0]).c_str(),
-                                rust_f64(ex.length[0]).c_str());
-                }
-                if (after) after(agent, legends()[i]);
-                rlamd::Histories e = agent.evaluate(n);
-                te_r.push_back(moving_average(maw ? n / maw : 0, e.reward));
-                te_l.push_back(moving_average(maw ? n / maw : 0, e.length));
-                ++i;
-                agent.reset();
+        if (spec.planning) rlamd::check(rl_agent_set_planning(agent.handle(), spec.planning), "rl_agent_set_planning");
+        for (const RunSpec &run : spec.runs) {
+            agent.set_action_selector(run.selector);
+            agent.set_future_q_value_func(run.algo);
+            const auto t0 = std::chrono::steady_clock::now();
+            rlamd::Histories h = agent.train(n, n / 10, want_td);
+            const auto el = std::chrono::steady_clock::now() - t0;
+            std::printf("%s %s\n", run.legend.c_str(),
+                        rust_duration(std::chrono::duration_cast<std::chrono::nanoseconds>(el)).c_str());
+            std::fflush(stdout);
+            legend.push_back(run.legend);
+            tr_e.push_back(moving_average(maw ? h.training_error.size() / maw : 0, h.training_error));
+            tr_r.push_back(moving_average(maw ? n / maw : 0, h.reward));
+            tr_l.push_back(moving_average(maw ? n / maw : 0, h.length));
+            if (f.on("show_example")) {            // Agent::example (src/agent.rs:143-163)
+                rlamd::Histories ex = agent.evaluate(1);
+                std::printf("episode reward %s\nterminated with %s steps\n", rust_f64(ex.reward[0]).c_str(),
+                            rust_f64(ex.length[0]).c_str());
             }
+            if (after) after(agent, run.legend);
+            rlamd::Histories e = agent.evaluate(n);
+            te_r.push_back(moving_average(maw ? n / maw : 0, e.reward));
+            te_l.push_back(moving_average(maw ? n / maw : 0, e.length));
+            agent.reset();
         }
     }
     const std::string dir = f.str("out_dir");
-    write_csv(dir, "Train Rewards", legends(), tr_r);
-    write_csv(dir, "Train Episodes Length", legends(), tr_l);
-    write_csv(dir, "Training Error", legends(), tr_e);
-    write_csv(dir, "Test Rewards", legends(), te_r);
-    write_csv(dir, "Test Episodes Length", legends(), te_l);
+    write_csv(dir, "Train Rewards", legend, tr_r);
+    write_csv(dir, "Train Episodes Length", legend, tr_l);
+    write_csv(dir, "Training Error", legend, tr_e);
+    write_csv(dir, "Test Rewards", legend, te_r);
+    write_csv(dir, "Test Episodes Length", legend, te_l);
     return 0;
+}
+
+// the 12-run sweep of frozen_lake / taxi / cliffwalking / blackjack (:171-216)
+inline int run_sweep(const Flags &f, const rl_env_config &env, const AfterTrain &after = nullptr) {
+    std::vector<AgentSpec> specs;
+    size_t i = 0;
+    for (int agent_kind : {RL_AGENT_ONE_STEP, RL_AGENT_TRACES}) {
+        AgentSpec a{agent_kind, 0, {}};
+        for (int sel : {RL_SEL_EPS_GREEDY, RL_SEL_UCB})
+            for (int algo : {RL_ALGO_SARSA, RL_ALGO_QLEARNING, RL_ALGO_EXPECTED_SARSA})
+                a.runs.push_back(RunSpec{legends()[i++], sel, algo});
+        specs.push_back(a);
+    }
+    return run_agents(f, env, specs, after);
 }
 
 inline int guarded(const std::function<int()> &fn) {

@@ -99,6 +99,7 @@ SIGNATURES = {
     "rl_agent_set_recording": (C.c_int, [_V, C.c_int32]),
     "rl_agent_take_records": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64)]),
     "rl_agent_set_episode_log": (C.c_int, [_V, C.c_uint32]),
+    "rl_agent_set_planning": (C.c_int, [_V, C.c_uint32]),
     "rl_agent_take_episodes": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64), _P(C.c_uint64)]),
     "rl_agent_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
     "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
@@ -334,6 +335,10 @@ class Agent:
         out = np.zeros(n.value, RECORD_DTYPE)
         check(lib().rl_agent_take_records(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out.reshape(-1, self.L)
+
+    def set_planning(self, planning_steps):
+        """InternalModelAgent + RandomModel (Dyna-Q); private mode only."""
+        check(lib().rl_agent_set_planning(self.h, planning_steps))
 
     def set_episode_log(self, capacity_per_lane):
         check(lib().rl_agent_set_episode_log(self.h, capacity_per_lane))

@@ -94,6 +94,11 @@ def lib():
         L.rlo_u64_to_uniform01.argtypes = [C.c_uint64]
         L.rlo_uniform_int_u64.restype = C.c_uint32
         L.rlo_uniform_int_u64.argtypes = [C.c_uint64, C.c_uint64, P(C.c_int)]
+        L.rlo_gen_index_u64.restype = C.c_uint64
+        L.rlo_gen_index_u64.argtypes = [C.c_uint64, C.c_uint64, P(C.c_int)]
+        L.rlo_faithful_set_planning.argtypes = [C.c_void_p, C.c_uint32]
+        L.rlo_batch_set_planning.restype = C.c_int
+        L.rlo_batch_set_planning.argtypes = [C.c_void_p, C.c_uint32]
         L.rlo_uniform_card_u32.restype = C.c_uint32
         L.rlo_uniform_card_u32.argtypes = [C.c_uint32, P(C.c_int)]
         L.rlo_blackjack_obs_id.restype = C.c_uint64
@@ -217,6 +222,9 @@ class Faithful:
     def set_record(self, on=True):
         lib().rlo_faithful_set_record(self.h, int(on))
 
+    def set_planning(self, n):
+        lib().rlo_faithful_set_planning(self.h, n)
+
     def train(self, n_episodes, eval_at=0):
         return lib().rlo_faithful_train(self.h, n_episodes, eval_at)
 
@@ -287,6 +295,9 @@ class Batch:
 
     def set_algo(self, a):
         lib().rlo_batch_set_algo(self.h, ALGO[a])
+
+    def set_planning(self, n):
+        assert lib().rlo_batch_set_planning(self.h, n) == 0, "Dyna planning needs group_size 1"
 
     @property
     def private(self):

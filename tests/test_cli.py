@@ -22,7 +22,12 @@ BIN = os.path.join(HOST, "bin")
 COMMON = ["show_example", "n_episodes", "learning_rate", "initial_epsilon", "exploration_time",
           "final_epsilon", "confidence_level", "discount_factor", "lambda_factor", "moving_average_window"]
 FLAGS = {"frozen_lake": COMMON + ["stochastic_env", "map", "max_steps"],
-         "taxi": COMMON + ["max_steps"], "cliffwalking": COMMON + ["max_steps"], "blackjack": COMMON}
+         "taxi": COMMON + ["max_steps"], "cliffwalking": COMMON + ["max_steps"],
+         "cliffwalking_model": COMMON + ["max_steps"], "blackjack": COMMON}
+
+SWEEP = [("one_step", 0, [(s, a) for s in ("eps_greedy", "ucb") for a in ("sarsa", "qlearning", "expected_sarsa")]),
+         ("traces", 0, [(s, a) for s in ("eps_greedy", "ucb") for a in ("sarsa", "qlearning", "expected_sarsa")])]
+MODEL = [("one_step", 0, [("eps_greedy", "qlearning")]), ("one_step", 10, [("eps_greedy", "qlearning")])]
 
 
 @pytest.fixture(scope="module")
@@ -72,56 +77,57 @@ def test_cli_fails_loudly_without_gpu(built, rl):
     assert r.returncode != 0 and "rl_agent_create" in r.stderr
 
 
-def _oracle_sweep(oracle, env_kw, n, maw, lanes=1):
+def _oracle_sweep(oracle, env_kw, n, maw, specs=SWEEP, lanes=1):
     """The bins' sequence on the oracle (lane 0 histories from step records)."""
     import oracle_ffi as O
     want = {k: [] for k in ("Train Rewards", "Train Episodes Length", "Training Error", "Test Rewards",
                             "Test Episodes Length")}
-    for agent in ("one_step", "traces"):
-        p = oracle.default_params(agent=agent, selector="eps_greedy", algo="sarsa", n_lanes=lanes, group_size=1,
+    for agent, planning, runs in specs:
+        p = oracle.default_params(agent=agent, selector=runs[0][0], algo=runs[0][1], n_lanes=lanes, group_size=1,
                                   sync_every=256, n_episodes_for_decay=n, **env_kw)
         b = O.Batch(p)
-        for sel in ("eps_greedy", "ucb"):
+        if planning:
+            b.set_planning(planning)
+        for sel, algo in runs:
             b.set_selector(sel)
-            for algo in ("sarsa", "qlearning", "expected_sarsa"):
-                b.set_algo(algo)
-                b.set_record(True)
-                b.train_episodes(n, n // 10)
-                recs = b.records()[:, 0]
-                b.set_record(False)
-                rew, ln, td = [], [], []
-                r, k = 0.0, 0
-                for x in recs:
-                    if x["kind"] == 1:
-                        r, k = 0.0, 0
-                    elif x["kind"] == 2:
-                        if x["mode"] == 0:
-                            td.append(float(x["td"]))
-                        r += float(x["r"])
-                        k += 1
-                        if x["term"] and x["mode"] == 0:
-                            rew.append(r)
-                            ln.append(float(k))
-                want["Training Error"].append(ref_moving_average(len(td) // maw, td))
-                want["Train Rewards"].append(ref_moving_average(n // maw, rew))
-                want["Train Episodes Length"].append(ref_moving_average(n // maw, ln))
-                b.set_record(True)
-                b.evaluate(n)
-                recs = b.records()[:, 0]
-                b.set_record(False)
-                rew, ln = [], []
-                for x in recs:
-                    if x["kind"] == 1:
-                        r, k = 0.0, 0
-                    elif x["kind"] == 2:
-                        r += float(x["r"])
-                        k += 1
-                        if x["term"]:
-                            rew.append(r)
-                            ln.append(float(k))
-                want["Test Rewards"].append(ref_moving_average(n // maw, rew))
-                want["Test Episodes Length"].append(ref_moving_average(n // maw, ln))
-                b.reset()
+            b.set_algo(algo)
+            b.set_record(True)
+            b.train_episodes(n, n // 10)
+            recs = b.records()[:, 0]
+            b.set_record(False)
+            rew, ln, td = [], [], []
+            r, k = 0.0, 0
+            for x in recs:
+                if x["kind"] == 1:
+                    r, k = 0.0, 0
+                elif x["kind"] == 2:
+                    if x["mode"] == 0:
+                        td.append(float(x["td"]))
+                    r += float(x["r"])
+                    k += 1
+                    if x["term"] and x["mode"] == 0:
+                        rew.append(r)
+                        ln.append(float(k))
+            want["Training Error"].append(ref_moving_average(len(td) // maw, td))
+            want["Train Rewards"].append(ref_moving_average(n // maw, rew))
+            want["Train Episodes Length"].append(ref_moving_average(n // maw, ln))
+            b.set_record(True)
+            b.evaluate(n)
+            recs = b.records()[:, 0]
+            b.set_record(False)
+            rew, ln = [], []
+            for x in recs:
+                if x["kind"] == 1:
+                    r, k = 0.0, 0
+                elif x["kind"] == 2:
+                    r += float(x["r"])
+                    k += 1
+                    if x["term"]:
+                        rew.append(r)
+                        ln.append(float(k))
+            want["Test Rewards"].append(ref_moving_average(n // maw, rew))
+            want["Test Episodes Length"].append(ref_moving_average(n // maw, ln))
+            b.reset()
     return want
 
 
@@ -133,18 +139,21 @@ def _read_csv(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prog,env_kw", [("frozen_lake", dict(env="frozen_lake", map8x8=0)),
-                                         ("cliffwalking", dict(env="cliff_walking"))])
-def test_cli_sweep_matches_oracle(built, oracle, tmp_path, prog, env_kw):
+@pytest.mark.parametrize("prog,env_kw,specs", [("frozen_lake", dict(env="frozen_lake", map8x8=0), SWEEP),
+                                               ("cliffwalking", dict(env="cliff_walking"), SWEEP),
+                                               ("cliffwalking_model", dict(env="cliff_walking"), MODEL)],
+                         ids=["frozen_lake", "cliffwalking", "cliffwalking_model"])
+def test_cli_sweep_matches_oracle(built, oracle, tmp_path, prog, env_kw, specs):
     n, maw = 40, 10
     out = subprocess.run([os.path.join(built, prog), "-n", str(n), "--moving_average_window", str(maw),
                           "--out_dir", str(tmp_path)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr
     lines = out.stdout.strip().split("\n")
-    assert len(lines) == 12 and lines[0].startswith("ε-Greedy One-Step Sarsa ")
-    want = _oracle_sweep(oracle, env_kw, n, maw)
+    n_runs = sum(len(r) for _, _, r in specs)
+    assert len(lines) == n_runs and lines[0].startswith("ε-Greedy One-Step ")
+    want = _oracle_sweep(oracle, env_kw, n, maw, specs)
     for title, series in want.items():
         header, got = _read_csv(os.path.join(tmp_path, title + ".csv"))
-        assert len(header) == 12
-        for j in range(12):
+        assert len(header) == n_runs
+        for j in range(n_runs):
             assert np.array_equal(np.array(got[j]), np.array(series[j]), equal_nan=True), (title, header[j])

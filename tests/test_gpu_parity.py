@@ -287,3 +287,34 @@ def test_episode_log_matches_oracle(rl, oracle, case):
     # interleave points 0, 10, 20 (episode % eval_at == 0, src/agent.rs:107)
     assert {sum(1 for g in got[l] if g[0] == 0) for l in range(L)} == {30}
     assert {sum(1 for g in got[l] if g[0] == 1) for l in range(L)} == {15}
+
+
+@pytest.mark.parametrize("case", [dict(env="cliff_walking", algo="qlearning"),
+                                  dict(env="taxi", selector="ucb", algo="expected_sarsa"),
+                                  dict(env="frozen_lake", map8x8=1, slippery=1, agent="traces",
+                                       policy="double", algo="sarsa"),
+                                  dict(env="blackjack", policy="double", algo="qlearning")],
+                         ids=["cw-q", "taxi-ucb-es", "fl-traces-double", "bj-double"])
+def test_dyna_matches_oracle(rl, oracle, case):
+    """InternalModelAgent + RandomModel, 10 planning steps (private agents):
+    records, Q, ε and stats bit-exact vs the oracle (itself == the faithful loop)."""
+    n = 40 if case["env"] != "blackjack" else 200
+    p = _params(rl, n_lanes=33, group_size=1, sync_every=29, n_episodes_for_decay=n, **case)
+    dev = rl.Agent(p)
+    dev.set_planning(10)
+    dev.set_recording(True)
+    ref = oracle.Batch(p)
+    ref.set_planning(10)
+    ref.set_record(True)
+    dev.train(n, n // 4)
+    ref.train_episodes(n, n // 4)
+    _assert_records_equal(dev.records(), ref.records())
+    _assert_q_equal(dev.q(), ref.q())
+    assert np.array_equal(dev.epsilon().view(np.uint64), ref.lane_eps().view(np.uint64))
+    _assert_stats_equal(dev, ref)
+    # Agent::reset empties the model too; a second run stays in lockstep
+    dev.reset()
+    ref.reset()
+    dev.train(n // 2, n // 4)
+    ref.train_episodes(n // 2, n // 4)
+    _assert_q_equal(dev.q(), ref.q())

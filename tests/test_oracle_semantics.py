@@ -141,3 +141,44 @@ def test_two_rank_merge_equals_one_process(oracle, case):
     for r in (0, 1):
         assert res[r][0] == ref_q
         assert res[r][1] == ref_n.tobytes() and res[r][2] == ref_t
+
+
+@pytest.mark.parametrize("kw", [dict(env="cliff_walking", algo="qlearning"),
+                                dict(env="taxi", selector="ucb", algo="expected_sarsa"),
+                                dict(env="frozen_lake", agent="traces", policy="double", algo="sarsa")],
+                         ids=["cw-q", "taxi-ucb-es", "fl-traces-double"])
+def test_dyna_private_batch_equals_faithful(oracle, kw):
+    """InternalModelAgent + RandomModel (src/agent/internal_model_agent.rs:47-77,
+    src/model/random_model.rs:27-40) with 10 planning steps: the batch's private
+    lanes reproduce the faithful Dyna loop bit for bit."""
+    n = 30
+    p = oracle.default_params(map8x8=1, n_episodes_for_decay=n, n_lanes=2, group_size=1, sync_every=41, **kw)
+    b = oracle.Batch(p)
+    b.set_planning(10)
+    b.train_episodes(n, n // 3)
+    q = b.q()
+    for lane in range(2):
+        f = oracle.Faithful(dict(p, lane_offset=lane))
+        f.set_planning(10)
+        f.train(n, n // 3)
+        assert _eq_nan(f.q(), q[lane])
+    # planning changes the result (the model is used; FrozenLake's Q stays 0
+    # until a goal is reached)
+    if kw["env"] != "frozen_lake":
+        b0 = oracle.Batch(p)
+        b0.train_episodes(n, n // 3)
+        assert not _eq_nan(b0.q(), q)
+
+
+def test_gen_range_index_kat(oracle):
+    """rand 0.8.5 sample_single_inclusive for usize: zone = (range << lz(range)) - 1."""
+    L = oracle.lib()
+    rej = __import__("ctypes").c_int()
+    # range 3: lz = 62, zone = 0xBFFF_FFFF_FFFF_FFFF; v * 3 = lo + hi * 2^64
+    v = 0x5555555555555556                       # v*3 = 2^64 + 2 -> hi 1, lo 2
+    assert L.rlo_gen_index_u64(v, 3, __import__("ctypes").byref(rej)) == 1 and rej.value == 0
+    v = 0x4000000000000000                       # v*3 = 0xC000...0 -> lo > zone: reject
+    L.rlo_gen_index_u64(v, 3, __import__("ctypes").byref(rej))
+    assert rej.value == 1
+    # range 4 (power of two): zone = 2^64 - 1, never rejects; index = top 2 bits
+    assert L.rlo_gen_index_u64(0xC000000000000000, 4, __import__("ctypes").byref(rej)) == 3 and rej.value == 0
