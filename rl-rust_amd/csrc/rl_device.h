@@ -251,7 +251,7 @@ struct EnvTables {
     const uint32_t *trans;
     const double *cdf;
     uint32_t n_start, max_steps;
-    double th1, th2, th3, trunc_reward;
+    double th1, th2, th3, trunc_reward;   // trunc_reward: host-side record only (the envs' own constants)
     int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
 };
 // Env::reset's categorical draw (frozen_lake.rs:107-108, taxi.rs:136-137): the
@@ -274,7 +274,7 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
-        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :119-122
+        if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :119-122
         z += 1;
         const uint32_t w = t.trans[pos * 4 + a];
         const double u = uniform01(r);                 // :126, drawn even when not slippery
@@ -299,7 +299,7 @@ template <> struct EnvDev<RL_ENV_CLIFF_WALKING> {
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
-        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :81-84
+        if (z >= t.max_steps) { s2 = 0; rew = -100.0; term = true; return; }  // :81-84
         z += 1;
         const uint32_t w = t.trans[pos * 4 + a];
         s2 = w & 63u;
@@ -321,7 +321,7 @@ template <> struct EnvDev<RL_ENV_TAXI> {
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
-        if (z >= t.max_steps) { s2 = 0; rew = t.trunc_reward; term = true; return; }  // :146-149
+        if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :146-149
         z += 1;
         const uint32_t w = t.trans[pos * 6 + a];
         s2 = w & 511u;

@@ -255,8 +255,10 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 }
 
 // ======================================================================== shared
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
-__global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
+// INSTR: step records / episode log compiled in (chosen at launch when either is
+// enabled); the throughput variant carries neither.
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
+__device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
     constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
@@ -485,18 +487,18 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
                 if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
             }
-            if (p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
+            if (INSTR && p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
             if (tr) atomicAdd(RSUM, (unsigned long long)(int64_t)__builtin_rint(L.epi_reward * 65536.0));
-            if (p.elog && (tr || ev)) log_episode(p, lane, L, tr);
+            if (INSTR && p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         } else if (doR) {
             L.s = s2;
             L.a = a2;
             L.need_reset = false;
             L.epi_reward = 0.0;
             L.epi_len = 0;
-            if (p.rec) write_record(p, k, lane, 1u, s2, a2, 0u, 0u, 0.0, false, 0.0, mode_before);
-        } else if (p.rec && active) {
+            if (INSTR && p.rec) write_record(p, k, lane, 1u, s2, a2, 0u, 0u, 0.0, false, 0.0, mode_before);
+        } else if (INSTR && p.rec && active) {
             write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
         }
         c_train += (uint32_t)__popcll(__ballot(train));
@@ -554,6 +556,23 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
             }
         }
     }
+}
+
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
+__global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, INSTR>(p);
+}
+// Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
+// learner groups whose LDS footprint allows 8 waves: one-step tabular
+// FrozenLake / CliffWalking.  The other variants would spill for no occupancy.
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false>(p);
+}
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+constexpr bool use_o8() {
+    return (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_CLIFF_WALKING) && AGENT == RL_AGENT_ONE_STEP &&
+           POLICY == RL_POLICY_TABULAR;
 }
 
 // ======================================================================== private
@@ -752,17 +771,22 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
 // ---------------------------------------------------------------- launch table
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int PRIV>
 hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream) {
-    const void *k = PRIV ? (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>
-                         : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO>;
+    const bool instr = p.rec != nullptr || p.elog != nullptr;
+    const void *k;
+    if constexpr (PRIV) {
+        k = (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>;
+    } else if (instr) {
+        k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, true>;
+    } else {
+        if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO>;
+        else k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+    }
     if (smem > 64 * 1024) {   // gfx950: a workgroup may use up to the CU's 160 KiB of LDS
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    if constexpr (PRIV)
-        hipLaunchKernelGGL((k_train_private<ENV, AGENT, POLICY, SEL, ALGO>), grid, block, smem, stream, p);
-    else
-        hipLaunchKernelGGL((k_train_shared<ENV, AGENT, POLICY, SEL, ALGO>), grid, block, smem, stream, p);
-    return hipGetLastError();
+    void *args[] = {(void *)&p};
+    return hipLaunchKernel(k, grid, block, args, smem, stream);
 }
 
 template <int ENV>

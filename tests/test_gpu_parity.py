@@ -318,3 +318,25 @@ def test_dyna_matches_oracle(rl, oracle, case):
     dev.train(n // 2, n // 4)
     ref.train_episodes(n // 2, n // 4)
     _assert_q_equal(dev.q(), ref.q())
+
+
+@pytest.mark.parametrize("case", [dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256),
+                                  dict(env="cliff_walking", algo="sarsa", group_size=64),
+                                  dict(env="taxi", selector="ucb", algo="expected_sarsa", group_size=128),
+                                  dict(env="blackjack", policy="double", algo="qlearning", group_size=256),
+                                  dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64)],
+                         ids=["fl-q-o8", "cw-sarsa-o8", "taxi-ucb-es", "bj-double", "cw-traces"])
+def test_throughput_variant_matches_oracle(rl, oracle, case):
+    """The kernels the bench runs (no records, no episode log: the INSTR=false
+    and occupancy-8 instantiations): raw Q, UCB counters and stats bit-exact."""
+    p = _params(rl, n_lanes=1500, sync_every=16, n_episodes_for_decay=40, **case)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    dev.run(5)
+    ref.run(5)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    if case.get("selector") == "ucb":
+        dn, dt = dev.ucb()
+        rn, rt = ref.ucb()
+        assert np.array_equal(dn, rn) and dt == rt
+    _assert_stats_equal(dev, ref)
