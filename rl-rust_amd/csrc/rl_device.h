@@ -30,6 +30,13 @@ struct Rng {
         s3 = __builtin_rotateleft32(s3, 11);
         return r;
     }
+    // advance as next_u32 does, without the output scrambler (a draw whose value is unused)
+    __device__ __forceinline__ void skip_u32() {
+        const uint32_t t = s1 << 9;
+        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3;
+        s2 ^= t;
+        s3 = __builtin_rotateleft32(s3, 11);
+    }
     // RngCore::next_u64 of a 32-bit block generator: low word first
     __device__ __forceinline__ uint64_t next_u64() {
         const uint64_t lo = next_u32();
@@ -253,6 +260,7 @@ struct EnvTables {
     uint32_t n_start, max_steps;
     double th1, th2, th3, trunc_reward;   // trunc_reward: host-side record only (the envs' own constants)
     int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
+    int32_t slippery;      // FrozenLake: the map has stochastic rows (uniform per launch)
 };
 // Env::reset's categorical draw (frozen_lake.rs:107-108, taxi.rs:136-137): the
 // uniform is always consumed; the search is skipped when the answer is fixed.
@@ -277,9 +285,14 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
         if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :119-122
         z += 1;
         const uint32_t w = t.trans[pos * 4 + a];
-        const double u = uniform01(r);                 // :126, drawn even when not slippery
         uint32_t i = 0;
-        if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
+        if (t.slippery) {                              // :126, drawn even when not slippery
+            const double u = uniform01(r);
+            if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
+        } else {
+            r.skip_u32();                              // deterministic map: the draw's value is unused
+            r.skip_u32();
+        }
         const uint32_t o = (w >> (8 * i)) & 0xffu;
         s2 = o & 63u;
         rew = (o & 64u) ? 1.0 : 0.0;

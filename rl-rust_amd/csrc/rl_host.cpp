@@ -45,6 +45,7 @@ struct EnvHost {
     std::vector<double> cdf;      // running sum of `start` (categorical_sample, utils.rs:33-43)
     double th1 = 0, th2 = 0, th3 = 0, trunc_reward = 0;
     int32_t fixed_start = -1;     // categorical_sample over `cdf` is constant (single start state)
+    int32_t slippery = 0;         // FrozenLake with stochastic rows
 };
 
 const char *const kFL4[] = {"SFFF", "FHFH", "FFFH", "HFFG"};                     // frozen_lake.rs:23
@@ -118,6 +119,7 @@ int build_env(const rl_env_config &c, EnvHost &e) {
                     else w = outcome(row, col, a);
                     e.trans[s * 4 + a] = w;
                 }
+        e.slippery = c.slippery ? 1 : 0;
         const double third = 1.0 / 3.0;
         e.th1 = 0.0 + third;
         e.th2 = e.th1 + third;
@@ -554,6 +556,7 @@ int rl_env_create(const rl_env_config *cfg, uint32_t n, uint64_t seed, uint64_t 
     p.core = e->core; p.rng = e->rng;
     p.trans = e->trans; p.start_cdf = e->cdf; p.n_start = (uint32_t)e->eh.cdf.size();
     p.fixed_start = e->eh.fixed_start;
+    p.slippery = e->eh.slippery;
     p.max_steps = e->eh.max_steps; p.th1 = e->eh.th1; p.th2 = e->eh.th2; p.th3 = e->eh.th3;
     p.trunc_reward = e->eh.trunc_reward;
     // lane init needs aux/epi_reward: use scratch
@@ -689,6 +692,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.trace = a->trace; p.tlist = a->tlist; p.slot_of = a->slot_of; p.tcnt = a->tcnt;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
     p.fixed_start = a->eh.fixed_start;
+    p.slippery = a->eh.slippery;
     p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
     p.trunc_reward = a->eh.trunc_reward;
     p.target_episodes = 0; p.eval_at = 0; p.eval_div = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;

@@ -64,6 +64,7 @@ struct KParams {
     const double *start_cdf;
     uint32_t n_start;
     int32_t fixed_start;   // >= 0 when the start distribution is a single state
+    int32_t slippery;      // FrozenLake with stochastic rows (else the per-step draw is skipped over)
     uint32_t max_steps;
     double th1, th2, th3;  // slippery FrozenLake cumulative sums
     double trunc_reward;

@@ -153,7 +153,7 @@ __global__ void k_env_reset(KParams p, uint64_t *obs) {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
     EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
-                p.fixed_start};
+                p.fixed_start, p.slippery};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};
@@ -168,7 +168,7 @@ __global__ void k_env_step(KParams p, const uint32_t *act, uint64_t *obs, double
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
     EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
-                p.fixed_start};
+                p.fixed_start, p.slippery};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};

@@ -305,6 +305,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
+    tabs.slippery = p.slippery;
 
     const uint64_t lane = (uint64_t)blockIdx.x * p.G + tid;
     const bool active = tid < p.G && lane < p.L;
@@ -605,6 +606,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
+    tabs.slippery = p.slippery;
 
     const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
     const bool active = lane < p.L;
