@@ -95,7 +95,7 @@ double rlo_log(double x) {
 /* RNG: the reference draws from rand::thread_rng() (ChaCha12, entropy       */
 /* seeded) at: frozen_lake.rs:156-157,175; taxi.rs:446-447; blackjack.rs:562 */
 /* (via :541); uniform_epsilon_greed.rs:51-54,62.  All sites share one        */
-/* thread-local stream.  Replacement: one xoshiro128** stream per lane,       */
+/* thread-local stream.  Replacement: one xoshiro128+ stream per lane,        */
 /* seeded by splitmix64(seed + lane*C); next_u64 = lo word then hi word.      */
 /* ======================================================================== */
 typedef struct { uint32_t s[4]; } rlo_rng;
@@ -114,9 +114,13 @@ static void rng_seed(rlo_rng *r, uint64_t seed, uint64_t lane) {
     if ((r->s[0] | r->s[1] | r->s[2] | r->s[3]) == 0) r->s[0] = 1;
 }
 static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+/* xoshiro128+ (Blackman & Vigna): every draw site consumes the high bits of its
+ * words (UniformFloat keeps bits 12..63 of next_u64, the integer mappings use the
+ * widening multiply's high word), where '+' is as good as '**' at a third of
+ * the output cost on the GPU. */
 static inline uint32_t next_u32(rlo_rng *r) {
     uint32_t *s = r->s;
-    uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+    uint32_t result = s[0] + s[3];
     uint32_t t = s[1] << 9;
     s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
     s[2] ^= t;

@@ -12,7 +12,7 @@
  * can be reproduced.  What IS pinned: hand-derived known-answer tests taken
  * from the reference source (tests/golden/tables.json["kat"]), and an independent Python
  * construction restatement of every transition table (tests/golden/tables.json).
- * The RNG stream (xoshiro128** per lane) replaces ThreadRng at exactly the
+ * The RNG stream (xoshiro128+ per lane) replaces ThreadRng at exactly the
  * reference's draw sites, with rand-0.8.5's distribution mappings restated.
  *
  * Two restatements live here:

@@ -19,11 +19,12 @@ constexpr double MIN_POSITIVE = 2.2250738585072014e-308;  // f64::MIN_POSITIVE
 
 // ------------------------------------------------------------------ RNG
 // Replaces rand::thread_rng() (entropy-seeded ChaCha12) at the reference's draw
-// sites with one xoshiro128** stream per lane, keyed (seed, global lane id).
+// sites with one xoshiro128+ stream per lane, keyed (seed, global lane id).  Every
+// draw site uses the words' high bits; '+' costs one VALU op of output mixing.
 struct Rng {
     uint32_t s0, s1, s2, s3;
     __device__ __forceinline__ uint32_t next_u32() {
-        const uint32_t r = __builtin_rotateleft32(s1 * 5u, 7) * 9u;
+        const uint32_t r = s0 + s3;
         const uint32_t t = s1 << 9;
         s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3;
         s2 ^= t;

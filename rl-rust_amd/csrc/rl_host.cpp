@@ -373,6 +373,7 @@ void agent_sync_params(rl_agent *a) {
 
 int launch_train_kernel(rl_agent *a) {
     agent_sync_params(a);
+    a->kp.episodic = (a->kp.target_episodes || a->kp.eval_at || a->kp.eval_only) ? 1 : 0;
     if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (a->timing) {

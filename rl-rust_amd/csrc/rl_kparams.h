@@ -76,6 +76,7 @@ struct KParams {
     uint64_t eval_div;     // ceil(2^64 / eval_at) (mod 2^64): divisibility test constant
     uint32_t eval_episodes;
     int32_t eval_only;
+    int32_t episodic;      // any of target_episodes / eval_at / eval_only set (else the run() fast path)
     // outputs
     unsigned long long *stats; // rl_stats as u64[8] x STATS_REP replicas (block b adds into b % STATS_REP)
     rl_step_record *rec;       // [K][L] or null

@@ -150,6 +150,17 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     L.a = a2;
     const bool tr = term && L.mode == RL_MODE_TRAIN;
     const bool ev = term && L.mode == RL_MODE_EVAL;
+    tr_out = tr;
+    ev_out = ev;
+    if (!p.episodic) {   // throughput mode (rl_agent_run): no target, no eval interleave;
+        // the general logic below reduces to exactly this
+        L.train_ep += tr ? 1u : 0u;
+        const uint32_t el = L.eval_left - (ev ? 1u : 0u);
+        L.mode = (ev && el == 0u) ? (uint32_t)RL_MODE_TRAIN : L.mode;
+        L.eval_left = el;
+        L.need_reset = L.need_reset || term;
+        return;
+    }
     const uint32_t ep = L.train_ep;                      // index of the episode that just ended
     const uint32_t new_ep = ep + (tr ? 1u : 0u);
     const bool go_eval = tr && p.eval_episodes != 0 && eval_hit(p, ep);   // episode % eval_at == 0
@@ -166,8 +177,6 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     L.train_ep = new_ep;
     L.eval_left = go_eval ? p.eval_episodes : el;
     L.need_reset = L.need_reset || term;
-    tr_out = tr;
-    ev_out = ev;
 }
 
 // episode log: reward_history / episode_length entries (src/agent.rs:96-100,

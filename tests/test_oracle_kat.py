@@ -131,7 +131,7 @@ def test_rng_stream_deterministic_and_lane_distinct(oracle):
     assert np.array_equal(a, oracle.rng_stream(0x5EED, 0, 1000))
     b = oracle.rng_stream(0x5EED, 1, 1000)
     assert (a != b).mean() > 0.99
-    # xoshiro128** words look uniform: mean of the top bit ~ 0.5
+    # xoshiro128+ words look uniform: mean of the top bit ~ 0.5
     w = oracle.rng_stream(7, 3, 100000)
     assert abs((w >> 31).mean() - 0.5) < 0.01
 
