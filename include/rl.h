@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1
+#define RL_ABI_VERSION 2
 
 enum rl_status {
     RL_OK = 0,
@@ -41,14 +41,32 @@ enum rl_status {
     RL_E_STATE = 5      /* call not valid in the handle's current mode */
 };
 
-enum rl_env_kind {      /* src/env/{frozen_lake,cliff_walking,taxi,blackjack}.rs */
-    RL_ENV_FROZEN_LAKE = 0, RL_ENV_CLIFF_WALKING = 1, RL_ENV_TAXI = 2, RL_ENV_BLACKJACK = 3
+enum rl_env_kind {      /* src/env/{frozen_lake,cliff_walking,taxi,blackjack,frozen_lake_edited}.rs */
+    RL_ENV_FROZEN_LAKE = 0, RL_ENV_CLIFF_WALKING = 1, RL_ENV_TAXI = 2, RL_ENV_BLACKJACK = 3,
+    RL_ENV_FROZEN_LAKE_EDITED = 4   /* FrozenLakeEditedEnv: obs = FrozenLakeObs, dense index = position */
 };
 enum rl_agent_kind {    /* src/agent/one_step_agent.rs, src/agent/elegibility_traces_agent.rs */
     RL_AGENT_ONE_STEP = 0, RL_AGENT_TRACES = 1
 };
-enum rl_policy_kind {   /* src/policy/tabular_policy.rs, src/policy/double_tabular_policy.rs */
-    RL_POLICY_TABULAR = 0, RL_POLICY_DOUBLE = 1
+enum rl_policy_kind {   /* src/policy/{tabular_policy,double_tabular_policy,neural_policy}.rs */
+    RL_POLICY_TABULAR = 0, RL_POLICY_DOUBLE = 1,
+    RL_POLICY_NEURAL = 2    /* NeuralPolicy over a 2-layer Network (src/policy/neural_policy.rs,
+                               src/network/); private mode (group_size 1) only */
+};
+/* Network activations (src/network/activation.rs); the pair (f, f') of each.
+ * RL_ACT_SOFTMAX normalises the whole layer and is accepted for the output layer only. */
+enum rl_activation {
+    RL_ACT_LINEAR = 0, RL_ACT_TANH = 1, RL_ACT_RELU = 2, RL_ACT_LEAKY_RELU = 3, RL_ACT_RELU6 = 4,
+    RL_ACT_LEAKY_RELU6 = 5, RL_ACT_SIGMOID = 6, RL_ACT_SOFTMAX = 7, RL_ACT_SWISH = 8,
+    RL_ACT_HARD_SWISH = 9
+};
+/* NeuralPolicy input adapters (InputAdapter<T> = fn(T) -> Array2<f64>, neural_policy.rs:9) */
+enum rl_input_adapter {
+    RL_INPUT_SCALAR = 0,  /* [[obs as f64]] of the reference's usize observation
+                             (src/bin/frozen_lake_neural.rs:147-149) */
+    RL_INPUT_FL_OBS = 1   /* [left, down, right, up terrain values, x, y] of FrozenLakeObs
+                             (frozen_lake_neural.rs:136-145; values frozen_lake_edited.rs:18-28);
+                             FrozenLake / FrozenLakeEdited only */
 };
 enum rl_selector_kind { /* src/action_selection/{uniform_epsilon_greed,upper_confidence_bound}.rs */
     RL_SEL_EPS_GREEDY = 0, RL_SEL_UCB = 1
@@ -72,6 +90,21 @@ typedef struct rl_env_config {
     uint32_t max_steps; /* truncation (frozen_lake.rs:119); ignored by Blackjack */
 } rl_env_config;
 
+/* NeuralPolicy::new(lr, input_adapter, network, output_adapter, inv_output_adapter)
+ * (src/policy/neural_policy.rs:20-35) with the bin's network shape
+ * (src/bin/frozen_lake_neural.rs:130-134): DenseLayer(n_in, hidden) -> act_hidden ->
+ * DenseLayer(hidden, COUNT) -> act_out, loss mse/mse_prime (src/network/loss.rs).
+ * The output adapters are the identity on COUNT values.  Ignored unless
+ * policy == RL_POLICY_NEURAL.  hidden <= RL_NET_MAX_HIDDEN. */
+#define RL_NET_MAX_HIDDEN 256
+#define RL_NET_MAX_INPUT 8
+typedef struct rl_network_config {
+    int32_t input;        /* rl_input_adapter */
+    uint32_t hidden;      /* 32 in the bin */
+    int32_t act_hidden;   /* rl_activation, RL_ACT_LEAKY_RELU6 in the bin */
+    int32_t act_out;      /* rl_activation, RL_ACT_LINEAR in the bin */
+} rl_network_config;
+
 /* Agent constructor arguments, gathered from the bins (src/bin/frozen_lake.rs:140-165):
  * OneStepAgent::new / ElegibilityTracesAgent::new + TabularPolicy::new(lr, default)
  * + UniformEpsilonGreed::new(eps0, decay, final) | UpperConfidenceBound::new(c). */
@@ -86,6 +119,7 @@ typedef struct rl_agent_config {
     uint32_t sync_every;  /* K: synchronous steps per launch; groups merge after every launch */
     uint32_t eval_episodes; /* episodes per in-train evaluate() (src/agent.rs:108 uses 100) */
     int32_t device;       /* HIP device ordinal */
+    rl_network_config net; /* policy == RL_POLICY_NEURAL only */
 } rl_agent_config;
 
 /* One per lane per synchronous step (recording mode only).  A live lane does
@@ -215,6 +249,18 @@ int rl_agent_take_episodes(rl_agent *a, rl_episode_record *out, uint64_t cap, ui
  * aux = {eps lo, eps hi, eval episodes left, episode length}; for checkpoints and tests */
 int rl_agent_lane_state(rl_agent *a, uint32_t *core, uint32_t *aux, size_t n_lanes);
 
+/* -------- NeuralPolicy weights (policy == RL_POLICY_NEURAL) */
+/* n_in = input features, n_params = per-lane parameter count:
+ * [W1 n_in x hidden][b1 hidden][W2 hidden x COUNT][b2 COUNT], row-major
+ * (DenseLayer::weights is (input_size, output_size), layers.rs:61-63) */
+int rl_agent_net_dims(rl_agent *a, uint32_t *n_in, uint32_t *hidden, uint32_t *n_params);
+/* all lanes' parameters, [n_lanes][n_params] f64 (Layer::get_weights / get_bias) */
+int rl_agent_get_weights(rl_agent *a, double *out, size_t n);
+/* Layer::set_weights / set_bias for every lane, same layout */
+int rl_agent_set_weights(rl_agent *a, const double *in, size_t n);
+/* the input-adapter features of every dense state, [n_states][n_in] (no GPU needed) */
+int rl_net_features(const rl_env_config *env, int32_t input, double *out, size_t n);
+
 /* -------- multi-GPU: the ΔQ merge as an external collective (shared mode) */
 /* number of int64 words of the merge delta (ΔQ, ΔN, Δt, Δflags) */
 int rl_agent_delta_words(rl_agent *a, uint64_t *n);
@@ -235,6 +281,9 @@ int rl_kat_log(int32_t device, const double *x, double *out, uint32_t n);
 int rl_kat_rng(int32_t device, uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out);
 int rl_kat_ucb(int32_t device, const double *q, const double *n_count, const uint64_t *t,
                double c, double *out, uint32_t n);
+/* activation f(x) and f'(x) on the device (src/network/activation.rs); act may
+ * not be RL_ACT_SOFTMAX (a layer-wide function, covered by the training tests) */
+int rl_kat_act(int32_t device, int32_t act, const double *x, double *f, double *fprime, uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -92,6 +92,163 @@ double rlo_log(double x) {
 }
 
 /* ======================================================================== */
+/* exp / expm1 / tanh: fdlibm e_exp.c, s_expm1.c, s_tanh.c operation         */
+/* sequences (public, Sun 1993).  The reference's activations call f64::exp / */
+/* f64::tanh (src/network/activation.rs:15-21,55-61,80-88), i.e. the platform */
+/* libm; as for ln, host and device evaluate this one sequence so the neural  */
+/* policy agrees bit for bit (tests/test_oracle_kat.py bounds it against      */
+/* numpy's libm to 1 ulp).                                                    */
+/* ======================================================================== */
+static inline uint32_t hi_word(double x) { dbits b; b.d = x; return (uint32_t)(b.u >> 32); }
+static inline uint32_t lo_word(double x) { dbits b; b.d = x; return (uint32_t)b.u; }
+static inline double with_hi(double x, uint32_t hi) {
+    dbits b; b.d = x; b.u = ((uint64_t)hi << 32) | (b.u & 0xffffffffull); return b.d;
+}
+static inline double add_exponent(double y, int k) {   /* __HI(y) += k << 20 */
+    return with_hi(y, (uint32_t)((int32_t)hi_word(y) + k * (1 << 20)));
+}
+
+double rlo_exp(double x) {
+    const double halF[2] = {0.5, -0.5}, huge = 1.0e+300, twom1000 = 9.33263618503218878990e-302,
+                 o_threshold = 7.09782712893383973096e+02, u_threshold = -7.45133219101941108420e+02,
+                 ln2HI[2] = {6.93147180369123816490e-01, -6.93147180369123816490e-01},
+                 ln2LO[2] = {1.90821492927058770002e-10, -1.90821492927058770002e-10},
+                 invln2 = 1.44269504088896338700e+00, P1 = 1.66666666666666019037e-01,
+                 P2 = -2.77777777770155933842e-03, P3 = 6.61375632143793436117e-05,
+                 P4 = -1.65339022054652515390e-06, P5 = 4.13813679705723846039e-08;
+    double y, hi = 0.0, lo = 0.0, c, t;
+    int k = 0;
+    uint32_t hx = hi_word(x);
+    const int xsb = (int)((hx >> 31) & 1u);
+    hx &= 0x7fffffffu;
+    if (hx >= 0x40862E42u) {
+        if (hx >= 0x7ff00000u) {
+            if (((hx & 0xfffffu) | lo_word(x)) != 0) return x + x;
+            return xsb == 0 ? x : 0.0;
+        }
+        if (x > o_threshold) return huge * huge;
+        if (x < u_threshold) return twom1000 * twom1000;
+    }
+    if (hx > 0x3fd62e42u) {
+        if (hx < 0x3FF0A2B2u) {
+            hi = x - ln2HI[xsb]; lo = ln2LO[xsb]; k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + halF[xsb]);
+            t = (double)k;
+            hi = x - t * ln2HI[0];
+            lo = t * ln2LO[0];
+        }
+        x = hi - lo;
+    } else if (hx < 0x3e300000u) {
+        if (huge + x > 1.0) return 1.0 + x;
+    } else {
+        k = 0;
+    }
+    t = x * x;
+    c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return add_exponent(y, k);
+    return add_exponent(y, k + 1000) * twom1000;
+}
+
+double rlo_expm1(double x) {
+    const double huge = 1.0e+300, tiny = 1.0e-300, o_threshold = 7.09782712893383973096e+02,
+                 ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00, Q1 = -3.33333333333331316428e-02,
+                 Q2 = 1.58730158725481460165e-03, Q3 = -7.93650757867487942473e-05,
+                 Q4 = 4.00821782732936239552e-06, Q5 = -2.01099218183624371326e-07;
+    double y, hi, lo, c = 0.0, t, e, hxs, hfx, r1;
+    int k;
+    uint32_t hx = hi_word(x);
+    const uint32_t xsb = hx & 0x80000000u;
+    hx &= 0x7fffffffu;
+    if (hx >= 0x4043687Au) {
+        if (hx >= 0x40862E42u) {
+            if (hx >= 0x7ff00000u) {
+                if (((hx & 0xfffffu) | lo_word(x)) != 0) return x + x;
+                return xsb == 0 ? x : -1.0;
+            }
+            if (x > o_threshold) return huge * huge;
+        }
+        if (xsb != 0) {
+            if (x + tiny < 0.0) return tiny - 1.0;
+        }
+    }
+    if (hx > 0x3fd62e42u) {
+        if (hx < 0x3FF0A2B2u) {
+            if (xsb == 0) { hi = x - ln2_hi; lo = ln2_lo; k = 1; }
+            else { hi = x + ln2_hi; lo = -ln2_lo; k = -1; }
+        } else {
+            k = (int)(invln2 * x + ((xsb == 0) ? 0.5 : -0.5));
+            t = (double)k;
+            hi = x - t * ln2_hi;
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+        c = (hi - x) - lo;
+    } else if (hx < 0x3c900000u) {
+        t = huge + x;
+        return x - (t - (huge + x));
+    } else {
+        k = 0;
+    }
+    hfx = 0.5 * x;
+    hxs = x * hfx;
+    r1 = 1.0 + hxs * (Q1 + hxs * (Q2 + hxs * (Q3 + hxs * (Q4 + hxs * Q5))));
+    t = 3.0 - r1 * hfx;
+    e = hxs * ((r1 - t) / (6.0 - x * t));
+    if (k == 0) return x - (x * e - hxs);
+    e = (x * (e - c) - c);
+    e -= hxs;
+    if (k == -1) return 0.5 * (x - e) - 0.5;
+    if (k == 1) {
+        if (x < -0.25) return -2.0 * (e - (x + 0.5));
+        return 1.0 + 2.0 * (x - e);
+    }
+    if (k <= -2 || k > 56) {
+        y = 1.0 - (e - x);
+        y = add_exponent(y, k);
+        return y - 1.0;
+    }
+    if (k < 20) {
+        t = with_hi(0.0, 0x3ff00000u - (0x200000u >> k));   /* 1 - 2^-k */
+        y = t - (e - x);
+        y = add_exponent(y, k);
+    } else {
+        t = with_hi(0.0, (uint32_t)((0x3ff - k) << 20));     /* 2^-k */
+        y = x - (e + t);
+        y += 1.0;
+        y = add_exponent(y, k);
+    }
+    return y;
+}
+
+double rlo_tanh(double x) {
+    const double tiny = 1.0e-300;
+    double t, z;
+    const int32_t jx = (int32_t)hi_word(x);
+    const int32_t ix = jx & 0x7fffffff;
+    if (ix >= 0x7ff00000) {
+        if (jx >= 0) return 1.0 / x + 1.0;
+        return 1.0 / x - 1.0;
+    }
+    if (ix < 0x40360000) {
+        if (ix < 0x3c800000) return x * (1.0 + x);
+        if (ix >= 0x3ff00000) {
+            t = rlo_expm1(2.0 * fabs(x));
+            z = 1.0 - 2.0 / (t + 2.0);
+        } else {
+            t = rlo_expm1(-2.0 * fabs(x));
+            z = -t / (t + 2.0);
+        }
+    } else {
+        z = 1.0 - tiny;
+    }
+    return jx >= 0 ? z : -z;
+}
+
+/* ======================================================================== */
 /* RNG: the reference draws from rand::thread_rng() (ChaCha12, entropy       */
 /* seeded) at: frozen_lake.rs:156-157,175; taxi.rs:446-447; blackjack.rs:562 */
 /* (via :541); uniform_epsilon_greed.rs:51-54,62.  All sites share one        */
@@ -283,6 +440,9 @@ typedef struct {
     double start[MAXS];
     uint32_t n_start;
     double trunc_reward;
+    int trunc_stay;      /* truncation observes the current position (FrozenLakeEdited) instead of 0 */
+    uint32_t nrow, ncol; /* grid envs */
+    const char **map;    /* FrozenLake maps */
 } envdef;
 
 typedef struct {
@@ -308,7 +468,7 @@ static void set_outcome(envdef *E, uint32_t s, uint32_t a, int i, double p, uint
 static void build_frozen_lake(envdef *E, int map8, int slippery) {
     const char **map = map8 ? FL8 : FL4;
     uint32_t n = map8 ? 8 : 4;
-    E->S = n * n; E->A = 4;
+    E->S = n * n; E->A = 4; E->nrow = E->ncol = n; E->map = map;
     uint32_t cnt = 0;
     for (uint32_t i = 0; i < E->S; ++i) if (map[i / n][i % n] == 'S') cnt++;
     for (uint32_t i = 0; i < E->S; ++i) E->start[i] = map[i / n][i % n] == 'S' ? 1.0 / (double)cnt : 0.0;
@@ -338,6 +498,73 @@ static void build_frozen_lake(envdef *E, int map8, int slippery) {
             }
         }
     E->trunc_reward = 0.0; /* frozen_lake.rs:119-122 */
+}
+
+/* FrozenLakeEditedEnv (src/env/frozen_lake_edited.rs).  Terrain of a cell
+ * (get_terrain :146-162) and of the neighbour in direction a, WALL off the map
+ * (get_obs :115-144); values (:18-28) feed the FL_OBS input adapter. */
+enum { T_START = 0, T_WALL = 1, T_HOLE = 2, T_GROUND = 3, T_GOAL = 4 };
+static int fl_terrain(const char **map, uint32_t row, uint32_t col) {
+    switch (map[row][col]) {
+    case 'S': return T_START;
+    case 'G': return T_GOAL;
+    case 'H': return T_HOLE;
+    default: return T_GROUND;
+    }
+}
+static int fl_neighbour(const char **map, uint32_t nrow, uint32_t ncol, uint32_t row, uint32_t col, uint32_t a) {
+    switch (a) {
+    case 0: return col == 0 ? T_WALL : fl_terrain(map, row, col - 1);
+    case 1: return row == nrow - 1 ? T_WALL : fl_terrain(map, row + 1, col);
+    case 2: return col == ncol - 1 ? T_WALL : fl_terrain(map, row, col + 1);
+    default: return row == 0 ? T_WALL : fl_terrain(map, row - 1, col);
+    }
+}
+static double fl_terrain_value(int t) {   /* FrozenLakeTerrain::value, frozen_lake_edited.rs:18-28 */
+    switch (t) {
+    case T_HOLE: return -1.0;
+    case T_WALL: return -0.5;
+    case T_START: return 0.0;
+    case T_GROUND: return 0.5;
+    default: return 1.0;
+    }
+}
+/* FrozenLakeEditedEnv::new (:165-218) + update_probability_matrix (:94-113):
+ * reward 10 for stepping onto G, else -1; terminated on G or H, judged by the
+ * terrain in the moved direction; G/H rows are (1.0, s, 0.0, true). */
+static void build_frozen_lake_edited(envdef *E, int map8, int slippery) {
+    const char **map = map8 ? FL8 : FL4;
+    uint32_t n = map8 ? 8 : 4;
+    E->S = n * n; E->A = 4; E->nrow = E->ncol = n; E->map = map;
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < E->S; ++i) if (map[i / n][i % n] == 'S') cnt++;
+    for (uint32_t i = 0; i < E->S; ++i) E->start[i] = map[i / n][i % n] == 'S' ? 1.0 / (double)cnt : 0.0;
+    E->n_start = E->S;
+    for (uint32_t row = 0; row < n; ++row)
+        for (uint32_t col = 0; col < n; ++col) {
+            uint32_t s = row * n + col;
+            for (uint32_t a = 0; a < 4; ++a) {
+                for (int i = 0; i < 3; ++i) set_outcome(E, s, a, i, 0.0, 0, 0.0, 0);
+                char letter = map[row][col];
+                if (letter == 'G' || letter == 'H') {
+                    set_outcome(E, s, a, 0, 1.0, s, 0.0, 1);
+                    continue;
+                }
+                uint32_t bs[3] = {(a + 3) % 4, a, (a + 1) % 4};   /* (a-1)%4 with usize wrap */
+                int nb = slippery ? 3 : 1;
+                for (int i = 0; i < nb; ++i) {
+                    uint32_t b = slippery ? bs[i] : a;
+                    int nt = fl_neighbour(map, n, n, row, col, b);
+                    uint32_t nr, nc;
+                    inc(n, n, row, col, b, &nr, &nc);
+                    int win = nt == T_GOAL;
+                    set_outcome(E, s, a, i, slippery ? 1.0 / 3.0 : 1.0, nr * n + nc, win ? 10.0 : -1.0,
+                                win || nt == T_HOLE);
+                }
+            }
+        }
+    E->trunc_reward = -1.0;   /* step :227-231: (obs of the current position, -1.0, true) */
+    E->trunc_stay = 1;
 }
 
 /* CliffWalkingEnv::new: src/env/cliff_walking.rs:22-58 */
@@ -403,6 +630,7 @@ static int build_env(envdef *E, const rlo_config *c) {
     E->max_steps = c->max_steps;
     switch (c->env) {
     case RLO_ENV_FROZEN_LAKE: build_frozen_lake(E, c->map8x8, c->slippery); return 0;
+    case RLO_ENV_FROZEN_LAKE_EDITED: build_frozen_lake_edited(E, c->map8x8, c->slippery); return 0;
     case RLO_ENV_CLIFF_WALKING: build_cliff_walking(E); return 0;
     case RLO_ENV_TAXI: build_taxi(E); return 0;
     case RLO_ENV_BLACKJACK: E->S = 32 * 27 * 2; E->A = 2; return 0;
@@ -494,15 +722,15 @@ static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint3
         else *rew = p > d ? 1.0 : (p < d ? -1.0 : 0.0);
         return 0;
     }
-    if (st->curr_step >= E->max_steps) {            /* truncation: (0, r_trunc, true) */
+    if (st->curr_step >= E->max_steps) {            /* truncation: (0 | pos, r_trunc, true) */
         st->ready = 0;
-        *s2 = 0; *rew = E->trunc_reward; *term = 1;
+        *s2 = E->trunc_stay ? st->pos : 0; *rew = E->trunc_reward; *term = 1;
         return 0;
     }
     st->curr_step += 1;
     size_t k = ((size_t)st->pos * E->A + a) * 3;
     uint32_t i = 0;
-    if (E->kind == RLO_ENV_FROZEN_LAKE) {
+    if (E->kind == RLO_ENV_FROZEN_LAKE || E->kind == RLO_ENV_FROZEN_LAKE_EDITED) {
         double u = uniform01(r);                       /* one draw even when not slippery */
         i = categorical_sample(&E->prob[k], 3, u);
     }
@@ -568,6 +796,215 @@ static double decay_eps(const rlo_config *c, double eps) {
 }
 
 /* ======================================================================== */
+/* NeuralPolicy over Network (src/policy/neural_policy.rs, src/network.rs,   */
+/* src/network/{layers,activation,loss}.rs).  Shape of the neural bin        */
+/* (src/bin/frozen_lake_neural.rs:130-134): DenseLayer(n_in, H) -> act1 ->   */
+/* DenseLayer(H, A) -> act2, mse.  Parameters [W1 n_in x H][b1 H][W2 H x A]  */
+/* [b2 A].  ndarray's dot (matrixmultiply dgemm) accumulates every output    */
+/* element over k in order from 0.0; that order is restated here WITHOUT      */
+/* fused multiply-add (dgemm's FMA use depends on the host CPU: parity with   */
+/* the Rust binary is unpinned; the GPU matches this restatement bit for bit).*/
+/* ======================================================================== */
+typedef struct { uint32_t in, H, A, np; int act1, act2; } netdef;
+static double max_rs(double a, double b) { return (a > b || b != b) ? a : b; }   /* f64::max */
+static double min_rs(double a, double b) { return (a < b || b != b) ? a : b; }   /* f64::min */
+static double sigmoid_(double v) { return 1.0 / (1.0 + rlo_exp(-v)); }
+/* activation.rs:5-94, elementwise pairs (softmax is layer-wide, see below) */
+static double act_f(int act, double v) {
+    switch (act) {
+    case RLO_ACT_TANH: return rlo_tanh(v);                                       /* :15-17 */
+    case RLO_ACT_RELU: return max_rs(v, 0.0);                                    /* :23-25 */
+    case RLO_ACT_LEAKY_RELU: return max_rs(v, 0.1 * v);                          /* :31-33 */
+    case RLO_ACT_RELU6: return min_rs(max_rs(v, 0.0), 6.0);                      /* :39-41 */
+    case RLO_ACT_LEAKY_RELU6: return min_rs(max_rs(v, 0.1 * v), 6.0);            /* :47-49 */
+    case RLO_ACT_SIGMOID: return sigmoid_(v);                                    /* :55-57 */
+    case RLO_ACT_SWISH: return v * sigmoid_(v);                                  /* :76-78 */
+    case RLO_ACT_HARD_SWISH: return (v * min_rs(max_rs(v + 3.0, 0.0), 6.0)) / 6.0; /* :84-86 */
+    default: return v;                                                           /* linear :7-9 */
+    }
+}
+static double act_fp(int act, double v) {
+    switch (act) {
+    case RLO_ACT_TANH: { double t = rlo_tanh(v); return 1.0 - t * t; }          /* :19-21 powf(2.0) */
+    case RLO_ACT_RELU: return v > 0.0 ? 1.0 : 0.0;                              /* :27-29 */
+    case RLO_ACT_LEAKY_RELU: return v > 0.0 ? 1.0 : 0.01;                       /* :35-37 */
+    case RLO_ACT_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.0;                /* :43-45 */
+    case RLO_ACT_LEAKY_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.01;         /* :51-53 */
+    case RLO_ACT_SIGMOID: { double sg = sigmoid_(v); return sg * (1.0 - sg); }  /* :59-62 */
+    case RLO_ACT_SWISH: {                                                       /* :80-82 */
+        double e = rlo_exp(v);
+        return (e * (v + e + 1.0)) / ((e + 1.0) * (e + 1.0));
+    }
+    case RLO_ACT_HARD_SWISH: return v > -3.0 ? (2.0 * v + 3.0) / 6.0 : 0.0;    /* :88-94 */
+    default: return 1.0;                                                        /* linear :11-13 */
+    }
+}
+void rlo_act(int32_t act, double x, double *f, double *fp) { *f = act_f(act, x); *fp = act_fp(act, x); }
+/* softmax (:64-74): e = exp(v - ndarray_max(v)) (utils.rs:23-31, strict >), e / e.sum();
+ * ndarray's sum is its eightfold unrolled fold (8 partial sums, then the tail).
+ * softmax_prime is the same function (as written, :70-74). */
+static void softmax_(const double *v, uint32_t n, double *out) {
+    double m = v[0], e[MAXA], acc = 0.0;
+    for (uint32_t i = 0; i < n; ++i) if (v[i] > m) m = v[i];
+    for (uint32_t i = 0; i < n; ++i) e[i] = rlo_exp(v[i] - m);
+    /* n = COUNT <= 6 < 8: the unrolled fold's partial sums stay 0.0 and the sum is
+     * the sequential tail 0.0 + e0 + e1 + ... */
+    for (uint32_t i = 0; i < n; ++i) acc = acc + e[i];
+    for (uint32_t k = 0; k < n; ++k) out[k] = e[k] / acc;
+}
+static void act_layer(int act, const double *v, uint32_t n, double *out) {
+    if (act == RLO_ACT_SOFTMAX) { softmax_(v, n, out); return; }
+    for (uint32_t i = 0; i < n; ++i) out[i] = act_f(act, v[i]);
+}
+static void act_layer_prime(int act, const double *v, uint32_t n, double *out) {
+    if (act == RLO_ACT_SOFTMAX) { softmax_(v, n, out); return; }
+    for (uint32_t i = 0; i < n; ++i) out[i] = act_fp(act, v[i]);
+}
+
+static int net_make(const rlo_config *c, uint32_t A, netdef *n) {
+    if (c->policy != RLO_POLICY_NEURAL) return -1;
+    n->in = c->net_input == RLO_INPUT_FL_OBS ? 6u : 1u;
+    n->H = c->net_hidden; n->A = A; n->act1 = c->net_act1; n->act2 = c->net_act2;
+    if (n->H == 0 || n->H > 256 || n->act1 == RLO_ACT_SOFTMAX || n->act1 < 0 || n->act1 > 9 ||
+        n->act2 < 0 || n->act2 > 9)
+        return -1;
+    if (c->net_input == RLO_INPUT_FL_OBS && c->env != RLO_ENV_FROZEN_LAKE && c->env != RLO_ENV_FROZEN_LAKE_EDITED)
+        return -1;
+    if (c->net_input == RLO_INPUT_SCALAR && c->env == RLO_ENV_FROZEN_LAKE_EDITED) return -1; /* struct obs */
+    n->np = n->in * n->H + n->H + n->H * A + A;
+    return 0;
+}
+/* input adapters: [[obs as f64]] (frozen_lake_neural.rs:147-149) of the reference
+ * observation id, or the FrozenLakeObs features (:136-145) */
+static void net_features(const envdef *E, const netdef *n, int input, double *feat) {
+    for (uint32_t s = 0; s < E->S; ++s) {
+        double *x = feat + (size_t)s * n->in;
+        if (input == RLO_INPUT_FL_OBS) {
+            uint32_t row = s / E->ncol, col = s % E->ncol;
+            for (uint32_t a = 0; a < 4; ++a)
+                x[a] = fl_terrain_value(fl_neighbour(E->map, E->nrow, E->ncol, row, col, a));
+            x[4] = (double)row;
+            x[5] = (double)col;
+        } else if (E->kind == RLO_ENV_BLACKJACK) {
+            x[0] = (double)rlo_blackjack_obs_id(s / 54u, (s >> 1) % 27u, s & 1u);
+        } else {
+            x[0] = (double)s;
+        }
+    }
+}
+/* forward: opre = pre-activation output layer, y = act2(opre).  Dense: x.dot(W) + b
+ * (layers.rs:78-81); Activation: f(input) (:130-133) */
+static void net_forward(const netdef *n, const double *w, const double *x, double *opre, double *y) {
+    const double *W1 = w, *b1 = w + n->in * n->H, *W2 = b1 + n->H, *b2 = W2 + (size_t)n->H * n->A;
+    double acc[MAXA];
+    for (uint32_t i = 0; i < n->A; ++i) acc[i] = 0.0;
+    for (uint32_t j = 0; j < n->H; ++j) {
+        double z = 0.0;
+        for (uint32_t k = 0; k < n->in; ++k) z = z + x[k] * W1[(size_t)k * n->H + j];
+        z = z + b1[j];
+        double h = act_f(n->act1, z);
+        for (uint32_t i = 0; i < n->A; ++i) acc[i] = acc[i] + h * W2[(size_t)j * n->A + i];
+    }
+    for (uint32_t i = 0; i < n->A; ++i) opre[i] = acc[i] + b2[i];
+    act_layer(n->act2, opre, n->A, y);
+}
+/* Network::fit (src/network.rs:61-80): forward, error = mse_prime (loss.rs:4-9:
+ * 2*(y_pred - y_true)/len), then backward through the layers in reverse
+ * (layers.rs:83-93, :135-141): Dense input_error = err.dot(W.t()) with the old W,
+ * W -= lr * input.t().dot(err), b -= lr * err. */
+static void net_fit(const netdef *n, double *w, const double *x, const double *target, double lr) {
+    double *W1 = w, *b1 = w + n->in * n->H, *W2 = b1 + n->H, *b2 = W2 + (size_t)n->H * n->A;
+    double opre[MAXA], y[MAXA], pr[MAXA], e2[MAXA];
+    net_forward(n, w, x, opre, y);
+    act_layer_prime(n->act2, opre, n->A, pr);
+    for (uint32_t i = 0; i < n->A; ++i) e2[i] = pr[i] * ((2.0 * (y[i] - target[i])) / (double)n->A);
+    for (uint32_t j = 0; j < n->H; ++j) {
+        double z = 0.0;
+        for (uint32_t k = 0; k < n->in; ++k) z = z + x[k] * W1[(size_t)k * n->H + j];
+        z = z + b1[j];
+        const double h = act_f(n->act1, z);
+        double ie = 0.0;
+        for (uint32_t i = 0; i < n->A; ++i) ie = ie + e2[i] * W2[(size_t)j * n->A + i];
+        for (uint32_t i = 0; i < n->A; ++i) {
+            double *wv = &W2[(size_t)j * n->A + i];
+            *wv = *wv - lr * (0.0 + h * e2[i]);
+        }
+        const double e1 = act_fp(n->act1, z) * ie;
+        for (uint32_t k = 0; k < n->in; ++k) {
+            double *wv = &W1[(size_t)k * n->H + j];
+            *wv = *wv - lr * (0.0 + x[k] * e1);
+        }
+        b1[j] = b1[j] - lr * e1;
+    }
+    for (uint32_t i = 0; i < n->A; ++i) b2[i] = b2[i] - lr * e2[i];
+}
+/* rand 0.8.5 UniformFloat::<f64>::new(low, high) scale (decrease until
+ * scale * max_rand + low < high) */
+static double uniform_scale(double low, double high) {
+    const double max_rand = 1.0 - 0x1p-52;
+    double scale = high - low;
+    while (scale * max_rand + low >= high) { dbits b; b.d = scale; b.u -= 1; scale = b.d; }
+    return scale;
+}
+/* weight stream of generation `gen` (0 = DenseLayer::new, k = the k-th Network::reset) */
+static uint64_t net_seed(uint64_t seed, uint32_t gen) { return seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(gen + 1u)); }
+/* DenseLayer::new (layers.rs:55-73): W ~ Uniform::new(-l, l), l = sqrt(6/(in+out)),
+ * drawn row-major, b = 0; DenseLayer::reset (:90-95): new W the same way, b = 0.1 */
+static void net_init(const netdef *n, double *w, uint64_t seed, uint64_t lane, uint32_t gen) {
+    rlo_rng r;
+    rng_seed(&r, net_seed(seed, gen), lane);
+    const uint32_t dims[2][2] = {{n->in, n->H}, {n->H, n->A}};
+    double *p = w;
+    for (int L = 0; L < 2; ++L) {
+        const uint32_t fi = dims[L][0], fo = dims[L][1];
+        const double l = sqrt(6.0 / (double)(fi + fo));
+        const double scale = uniform_scale(-l, l);
+        for (uint32_t k = 0; k < fi * fo; ++k) {
+            dbits b; b.u = (next_u64(&r) >> 12) | 0x3FF0000000000000ull;
+            p[k] = (b.d - 1.0) * scale + -l;
+        }
+        p += fi * fo;
+        for (uint32_t k = 0; k < fo; ++k) p[k] = gen ? 0.1 : 0.0;
+        p += fo;
+    }
+}
+int rlo_net_dims(const rlo_config *c, uint32_t *n_in, uint32_t *n_params) {
+    envdef *E = (envdef *)malloc(sizeof(envdef));
+    netdef n;
+    int rc = build_env(E, c) || net_make(c, E->A, &n) ? -1 : 0;
+    if (!rc) { *n_in = n.in; *n_params = n.np; }
+    free(E);
+    return rc;
+}
+int rlo_net_features(const rlo_config *c, double *out) {
+    envdef *E = (envdef *)malloc(sizeof(envdef));
+    netdef n;
+    int rc = build_env(E, c) || net_make(c, E->A, &n) ? -1 : 0;
+    if (!rc) net_features(E, &n, c->net_input, out);
+    free(E);
+    return rc;
+}
+void rlo_net_init(const rlo_config *c, uint64_t lane, uint32_t gen, double *w) {
+    envdef *E = (envdef *)malloc(sizeof(envdef));
+    netdef n;
+    if (!build_env(E, c) && !net_make(c, E->A, &n)) net_init(&n, w, c->seed, lane, gen);
+    free(E);
+}
+void rlo_net_forward(const rlo_config *c, const double *w, const double *x, double *y) {
+    envdef *E = (envdef *)malloc(sizeof(envdef));
+    netdef n;
+    double opre[MAXA];
+    if (!build_env(E, c) && !net_make(c, E->A, &n)) net_forward(&n, w, x, opre, y);
+    free(E);
+}
+void rlo_net_fit(const rlo_config *c, double *w, const double *x, const double *y_target, double lr) {
+    envdef *E = (envdef *)malloc(sizeof(envdef));
+    netdef n;
+    if (!build_env(E, c) && !net_make(c, E->A, &n)) net_fit(&n, w, x, y_target, lr);
+    free(E);
+}
+
+/* ======================================================================== */
 /* 1. faithful single-env restatement                                        */
 /* ======================================================================== */
 typedef struct { void *p; size_t n, cap, esz; } vec;
@@ -593,6 +1030,10 @@ struct rlo_faithful {
     uint64_t ucb_t;
     double *trace;       /* [S][A] */
     uint8_t *visited;    /* [S] — membership of the trace FxHashMap */
+    uint32_t *vlist, vcnt; /* visited states in first-visit order (the sweep order, see f_update) */
+    netdef net;          /* NeuralPolicy */
+    double *w, *feat;    /* parameters [np], input features [S][in] */
+    uint32_t net_gen;    /* Network::reset calls so far */
     vec reward_history, episode_length, training_error, records;
     int record;
     uint32_t plan;       /* InternalModelAgent planning steps (0: plain agent) */
@@ -600,6 +1041,7 @@ struct rlo_faithful {
 };
 
 static void f_clear_policy(rlo_faithful *f) {
+    if (f->w) { net_init(&f->net, f->w, f->c.seed, f->c.lane_offset, ++f->net_gen); return; }  /* Network::reset */
     for (size_t i = 0; i < (size_t)f->P * f->S * f->A; ++i) f->q[i] = f->c.q_default;
 }
 static void f_reset_selector(rlo_faithful *f) {
@@ -617,12 +1059,20 @@ rlo_faithful *rlo_faithful_create(const rlo_config *c) {
     f->ucb_n = (uint64_t *)calloc((size_t)f->S * f->A, sizeof(uint64_t));
     f->trace = (double *)calloc((size_t)f->S * f->A, sizeof(double));
     f->visited = (uint8_t *)calloc(f->S, 1);
+    f->vlist = (uint32_t *)calloc(f->S, sizeof(uint32_t));
+    if (c->policy == RLO_POLICY_NEURAL) {
+        if (net_make(c, f->A, &f->net)) { free(f->q); free(f->ucb_n); free(f->trace); free(f->visited); free(f->vlist); free(f); return NULL; }
+        f->w = (double *)malloc(sizeof(double) * f->net.np);
+        f->feat = (double *)malloc(sizeof(double) * f->S * f->net.in);
+        net_features(&f->E, &f->net, c->net_input, f->feat);
+    }
     f->reward_history.esz = sizeof(double);
     f->episode_length.esz = sizeof(uint64_t);
     f->training_error.esz = sizeof(double);
     f->records.esz = sizeof(rlo_record);
     f->dflag = 1;
-    f_clear_policy(f);
+    if (f->w) net_init(&f->net, f->w, c->seed, c->lane_offset, 0);   /* NeuralPolicy::new */
+    else f_clear_policy(f);
     f_reset_selector(f);
     rng_seed(&f->rng, c->seed, c->lane_offset);
     if (c->env == RLO_ENV_BLACKJACK) bj_initialize_hands(&f->st, &f->rng); /* BlackJackEnv::new deals */
@@ -630,7 +1080,7 @@ rlo_faithful *rlo_faithful_create(const rlo_config *c) {
 }
 void rlo_faithful_destroy(rlo_faithful *f) {
     if (!f) return;
-    free(f->q); free(f->ucb_n); free(f->trace); free(f->visited);
+    free(f->q); free(f->ucb_n); free(f->trace); free(f->visited); free(f->vlist); free(f->w); free(f->feat);
     free(f->reward_history.p); free(f->episode_length.p); free(f->training_error.p); free(f->records.p);
     model_free(&f->model);
     free(f);
@@ -638,20 +1088,32 @@ void rlo_faithful_destroy(rlo_faithful *f) {
 void rlo_faithful_set_record(rlo_faithful *f, int e) { f->record = e; }
 double rlo_faithful_epsilon(const rlo_faithful *f) { return f->eps; }
 
-/* Policy::predict: tabular_policy.rs:27-29, double_tabular_policy.rs:31-40 */
+/* Policy::predict: tabular_policy.rs:27-29, double_tabular_policy.rs:31-40,
+ * neural_policy.rs:43-47 (input adapter, Network::predict, output adapter) */
 static void f_predict(const rlo_faithful *f, uint32_t s, double *out) {
+    if (f->w) { double opre[MAXA]; net_forward(&f->net, f->w, f->feat + (size_t)s * f->net.in, opre, out); return; }
     const double *a = &f->q[(size_t)s * f->A];
     if (f->P == 1) { for (uint32_t i = 0; i < f->A; ++i) out[i] = a[i]; return; }
     const double *b = &f->q[((size_t)f->S + s) * f->A];
     for (uint32_t i = 0; i < f->A; ++i) out[i] = (a[i] + b[i]) / 2.0;
 }
-/* Policy::get_values: tabular_policy.rs:31-33, double_tabular_policy.rs:42-50 (flag ? alpha : beta) */
-static const double *f_values(const rlo_faithful *f, uint32_t s) {
+/* Policy::get_values: tabular_policy.rs:31-33, double_tabular_policy.rs:42-50 (flag ? alpha : beta),
+ * neural_policy.rs:49-53 */
+static void f_values(const rlo_faithful *f, uint32_t s, double *out) {
+    if (f->w) { f_predict(f, s, out); return; }
     uint32_t tbl = (f->P == 2 && !f->dflag) ? 1 : 0;
-    return &f->q[((size_t)tbl * f->S + s) * f->A];
+    memcpy(out, &f->q[((size_t)tbl * f->S + s) * f->A], f->A * sizeof(double));
 }
-/* Policy::update: tabular_policy.rs:35-38, double_tabular_policy.rs:52-60 (flag ? beta : alpha) */
+/* Policy::update: tabular_policy.rs:35-38, double_tabular_policy.rs:52-60 (flag ? beta : alpha);
+ * neural_policy.rs:55-62: y = get_values(s), y[a] += td, Network::fit(x(s), y, lr) */
 static void f_policy_update(rlo_faithful *f, uint32_t s, uint32_t a, double td) {
+    if (f->w) {
+        double y[MAXA];
+        f_values(f, s, y);
+        y[a] += td;
+        net_fit(&f->net, f->w, f->feat + (size_t)s * f->net.in, y, f->c.lr);
+        return;
+    }
     uint32_t tbl = (f->P == 2 && f->dflag) ? 1 : 0;
     f->q[((size_t)tbl * f->S + s) * f->A + a] += f->c.lr * td;
 }
@@ -677,19 +1139,21 @@ static double f_update(rlo_faithful *f, uint32_t s, uint32_t a, double r, int te
                        uint32_t a2) {
     const uint32_t A = f->A;
     double q2[MAXA], p[MAXA], q[MAXA];
-    memcpy(q2, f_values(f, s2), A * sizeof(double));
+    f_values(f, s2, q2);
     if (f->c.selector == RLO_SEL_EPS_GREEDY) eps_probs(f->eps, q2, A, p);
     else ucb_probs(q2, &f->ucb_n[(size_t)s2 * A], f->ucb_t, f->c.ucb_c, A, p);
     double fq = future_q(f->c.algo, q2, a2, p, A);
-    memcpy(q, f_values(f, s), A * sizeof(double));
+    f_values(f, s, q);
     double td = r + f->c.gamma * fq - q[a];
     if (f->c.agent == RLO_AGENT_ONE_STEP) {
         f_policy_update(f, s, a, td);
     } else {
         f->trace[(size_t)s * A + a] += 1.0;
-        f->visited[s] = 1;
-        for (uint32_t o = 0; o < f->S; ++o) {
-            if (!f->visited[o]) continue;
+        if (!f->visited[s]) { f->visited[s] = 1; f->vlist[f->vcnt++] = s; }
+        /* the reference sweeps its FxHashMap; tabular updates are order-free, the
+         * neural policy's are not: the sweep runs in first-visit order (as the GPU) */
+        for (uint32_t vi = 0; vi < f->vcnt; ++vi) {
+            const uint32_t o = f->vlist[vi];
             for (uint32_t b = 0; b < A; ++b) {
                 double *e = &f->trace[(size_t)o * A + b];
                 f_policy_update(f, o, b, td * *e);
@@ -702,6 +1166,7 @@ static double f_update(rlo_faithful *f, uint32_t s, uint32_t a, double r, int te
         if (f->c.agent == RLO_AGENT_TRACES) {
             memset(f->trace, 0, sizeof(double) * f->S * A);
             memset(f->visited, 0, f->S);
+            f->vcnt = 0;
         }
         if (f->c.selector == RLO_SEL_EPS_GREEDY) f->eps = decay_eps(&f->c, f->eps);
     }
@@ -783,7 +1248,14 @@ uint64_t rlo_faithful_train(rlo_faithful *f, uint64_t n_episodes, uint64_t eval_
 /* Agent::reset (one_step_agent.rs:43-46): selector.reset + policy.reset (flag kept) */
 void rlo_faithful_reset(rlo_faithful *f) { f_reset_selector(f); f_clear_policy(f); f->model.cnt = 0; }
 void rlo_faithful_get_q(const rlo_faithful *f, double *out) {
+    if (f->w) { for (uint32_t s = 0; s < f->S; ++s) f_values(f, s, out + (size_t)s * f->A); return; }
     memcpy(out, f->q, sizeof(double) * f->P * f->S * f->A);
+}
+void rlo_faithful_get_weights(const rlo_faithful *f, double *out) {
+    if (f->w) memcpy(out, f->w, sizeof(double) * f->net.np);
+}
+void rlo_faithful_set_weights(rlo_faithful *f, const double *in) {
+    if (f->w) memcpy(f->w, in, sizeof(double) * f->net.np);
 }
 uint64_t rlo_faithful_n_episodes(const rlo_faithful *f) { return f->reward_history.n; }
 uint64_t rlo_faithful_n_steps(const rlo_faithful *f) { return f->training_error.n; }
@@ -827,6 +1299,8 @@ typedef struct {
     double eps, epi_reward;
     uint64_t train_ep, eval_left, epi_len;
     double *trace;       /* [S][A] (traces agent) */
+    uint32_t *vlist, vcnt; /* visited states in first-visit order */
+    double *w;           /* NeuralPolicy parameters (private mode) */
     uint8_t *visited;
     /* private mode (G == 1): the lane is a whole reference agent */
     double *qd;          /* [P][S][A] f64 */
@@ -861,6 +1335,9 @@ struct rlo_batch {
     vec records;
     uint64_t stats[8];
     uint32_t plan;       /* Dyna planning steps per update (private mode only) */
+    netdef net;          /* NeuralPolicy (private mode only) */
+    double *feat, *w_g;  /* input features [S][in]; current lane's parameters */
+    uint32_t net_gen;
 };
 
 /* Fixed-point Q (shared mode).  |Q raw| <= 2^52, so every entry converts to
@@ -893,6 +1370,11 @@ static inline int64_t wrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_
 
 static void b_row(const rlo_batch *b, uint32_t tbl, uint32_t s, double *out) {
     size_t base = ((size_t)tbl * b->S + s) * b->A;
+    if (b->feat) {                    /* NeuralPolicy::get_values / predict (neural_policy.rs:43-53) */
+        double opre[MAXA];
+        net_forward(&b->net, b->w_g, b->feat + (size_t)s * b->net.in, opre, out);
+        return;
+    }
     if (b->priv) {
         for (uint32_t i = 0; i < b->A; ++i) out[i] = b->qd_g[base + i];
         return;
@@ -946,6 +1428,11 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
     b->specials = c->selector == RLO_SEL_UCB && c->algo == RLO_ALGO_EXPECTED_SARSA;
     b->priv = b->G == 1;
     if (b->G > 1024) { free(b); return NULL; }
+    if (c->policy == RLO_POLICY_NEURAL) {
+        if (!b->priv || net_make(c, b->A, &b->net)) { free(b); return NULL; }
+        b->feat = (double *)malloc(sizeof(double) * b->S * b->net.in);
+        net_features(&b->E, &b->net, c->net_input, b->feat);
+    }
     size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
     b->q_base = (int64_t *)malloc(nq * 8); b->f_base = (uint8_t *)calloc(nq, 1);
     b->q_g = (int64_t *)malloc(nq * 8); b->f_g = (uint8_t *)calloc(nq, 1);
@@ -961,13 +1448,16 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
         if (c->agent == RLO_AGENT_TRACES) {
             b->lanes[i].trace = (double *)calloc(nsa, sizeof(double));
             b->lanes[i].visited = (uint8_t *)calloc(b->S, 1);
+            b->lanes[i].vlist = (uint32_t *)calloc(b->S, sizeof(uint32_t));
         }
+        if (b->feat) b->lanes[i].w = (double *)malloc(sizeof(double) * b->net.np);
         if (b->priv) {
             b->lanes[i].qd = (double *)malloc(nq * sizeof(double));
             b->lanes[i].n = (uint32_t *)calloc(nsa, sizeof(uint32_t));
         }
         lane_init(b, &b->lanes[i], c->lane_offset + i);
     }
+    b->net_gen = (uint32_t)-1;           /* the first reset is NeuralPolicy::new (generation 0) */
     rlo_batch_reset(b);
     return b;
 }
@@ -975,11 +1465,12 @@ void rlo_batch_destroy(rlo_batch *b) {
     if (!b) return;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
         free(b->lanes[i].trace); free(b->lanes[i].visited); free(b->lanes[i].qd); free(b->lanes[i].n);
+        free(b->lanes[i].vlist); free(b->lanes[i].w);
         model_free(&b->lanes[i].model);
     }
     free(b->lanes); free(b->q_base); free(b->f_base); free(b->q_g); free(b->f_g); free(b->dq);
     free(b->df); free(b->dc); free(b->acc_c); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
-    free(b->records.p);
+    free(b->records.p); free(b->feat);
     free(b);
 }
 /* Agent::reset: policy cleared to the default row, selector state fresh, lane
@@ -992,9 +1483,11 @@ void rlo_batch_reset(rlo_batch *b) {
     for (size_t i = 0; i < nq; ++i) { b->q_base[i] = d; b->f_base[i] = fl; }
     memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
     b->t_base = 1;
+    b->net_gen++;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
         lane_t *L = &b->lanes[i];
         L->eps = b->c.eps0;
+        if (L->w) net_init(&b->net, L->w, b->c.seed, b->c.lane_offset + i, b->net_gen);  /* Network::reset */
         if (b->priv) {
             for (size_t k = 0; k < nq; ++k) L->qd[k] = b->c.q_default;
             memset(L->n, 0, sizeof(uint32_t) * b->S * b->A);
@@ -1053,6 +1546,20 @@ static int64_t mean_delta(int64_t sum, int64_t n) {
     return (int64_t)trunc((double)sum * (1.0 / (double)n));
 }
 
+/* Policy::update with x = td (one-step) or td * E[o][b] (traces):
+ * tabular Q[s][a] += lr * x; neural y = get_values(s), y[a] += x, fit */
+static void b_policy_update(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double x) {
+    if (b->feat) {
+        double y[MAXA], opre[MAXA];
+        const double *in = b->feat + (size_t)s * b->net.in;
+        net_forward(&b->net, b->w_g, in, opre, y);
+        y[a] += x;
+        net_fit(&b->net, b->w_g, in, y, b->c.lr);
+        return;
+    }
+    add_delta(b, tbl, s, a, b->c.lr * x);
+}
+
 /* Agent::update of one lane against the current Q / UCB state
  * (one_step_agent.rs:53-86, elegibility_traces_agent.rs:61-104), with
  * after_update and the termination hooks */
@@ -1074,16 +1581,16 @@ static double b_update(rlo_batch *b, lane_t *L, uint32_t s, uint32_t a, double r
     b_row(b, vt, s, q);
     double td = r + b->c.gamma * fq - q[a];
     if (b->c.agent == RLO_AGENT_ONE_STEP) {
-        add_delta(b, ut, s, a, b->c.lr * td);
+        b_policy_update(b, ut, s, a, td);
     } else {
         L->trace[(size_t)s * A + a] += 1.0;
-        L->visited[s] = 1;
-        for (uint32_t o = 0; o < b->S; ++o) {
-            if (!L->visited[o]) continue;
+        if (!L->visited[s]) { L->visited[s] = 1; L->vlist[L->vcnt++] = s; }
+        for (uint32_t vi = 0; vi < L->vcnt; ++vi) {   /* first-visit order (see f_update) */
+            const uint32_t o = L->vlist[vi];
             b->stats[7]++;                    /* visited-set entries swept (V per step) */
             for (uint32_t bb = 0; bb < A; ++bb) {
                 double *e = &L->trace[(size_t)o * A + bb];
-                add_delta(b, ut, o, bb, b->c.lr * (td * *e));
+                b_policy_update(b, ut, o, bb, td * *e);
                 *e *= b->c.gamma * b->c.lambda_;
             }
         }
@@ -1093,6 +1600,7 @@ static double b_update(rlo_batch *b, lane_t *L, uint32_t s, uint32_t a, double r
         if (b->c.agent == RLO_AGENT_TRACES) {
             memset(L->trace, 0, sizeof(double) * b->S * A);
             memset(L->visited, 0, b->S);
+            L->vcnt = 0;
         }
         if (!ucb) L->eps = decay_eps(&b->c, L->eps);
     }
@@ -1231,7 +1739,7 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
     if (b->priv) {
         for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
             lane_t *L = &b->lanes[i];
-            b->qd_g = L->qd; b->n_g = L->n; b->t_g = L->t;
+            b->qd_g = L->qd; b->n_g = L->n; b->t_g = L->t; b->w_g = L->w;
             for (uint32_t k = 0; k < b->K; ++k) {
                 group_step(b, i, 1, tmp);
                 if (tmp) ((rlo_record *)b->records.p)[rec0 + (size_t)k * b->c.n_lanes + i] = tmp[0];
@@ -1307,7 +1815,7 @@ uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n, uint64_t eval_at) {
         lane_t *L = &b->lanes[i];
         L->need_reset = 1; L->train_ep = 0; L->eval_left = 0;
         L->mode = n ? RLO_MODE_TRAIN : RLO_MODE_DONE;
-        if (L->trace) { memset(L->trace, 0, sizeof(double) * b->S * b->A); memset(L->visited, 0, b->S); }
+        if (L->trace) { memset(L->trace, 0, sizeof(double) * b->S * b->A); memset(L->visited, 0, b->S); L->vcnt = 0; }
     }
     uint64_t launches = 0;
     while (!all_done(b)) { run_launch(b); launches++; }
@@ -1329,6 +1837,13 @@ uint64_t rlo_batch_evaluate(rlo_batch *b, uint64_t n) {
 }
 void rlo_batch_get_q(const rlo_batch *b, double *out) {
     size_t nq = (size_t)b->P * b->S * b->A;
+    if (b->feat) {        /* [L][1][S][A] get_values of every state */
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+            ((rlo_batch *)b)->w_g = b->lanes[i].w;
+            for (uint32_t st = 0; st < b->S; ++st) b_row(b, 0, st, out + i * nq + (size_t)st * b->A);
+        }
+        return;
+    }
     if (b->priv) {        /* [L][P][S][A] */
         for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(out + i * nq, b->lanes[i].qd, nq * sizeof(double));
         return;
@@ -1368,4 +1883,13 @@ void rlo_batch_stats(const rlo_batch *b, uint64_t *out8) {
 }
 void rlo_batch_lane_eps(const rlo_batch *b, double *out) {
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) out[i] = b->lanes[i].eps;
+}
+
+void rlo_batch_get_weights(const rlo_batch *b, double *out) {
+    if (!b->feat) return;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(out + (size_t)i * b->net.np, b->lanes[i].w, sizeof(double) * b->net.np);
+}
+void rlo_batch_set_weights(rlo_batch *b, const double *in) {
+    if (!b->feat) return;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(b->lanes[i].w, in + (size_t)i * b->net.np, sizeof(double) * b->net.np);
 }

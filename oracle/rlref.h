@@ -38,9 +38,15 @@
 extern "C" {
 #endif
 
-enum { RLO_ENV_FROZEN_LAKE = 0, RLO_ENV_CLIFF_WALKING = 1, RLO_ENV_TAXI = 2, RLO_ENV_BLACKJACK = 3 };
+enum { RLO_ENV_FROZEN_LAKE = 0, RLO_ENV_CLIFF_WALKING = 1, RLO_ENV_TAXI = 2, RLO_ENV_BLACKJACK = 3,
+       RLO_ENV_FROZEN_LAKE_EDITED = 4 };
 enum { RLO_AGENT_ONE_STEP = 0, RLO_AGENT_TRACES = 1 };
-enum { RLO_POLICY_TABULAR = 0, RLO_POLICY_DOUBLE = 1 };
+enum { RLO_POLICY_TABULAR = 0, RLO_POLICY_DOUBLE = 1, RLO_POLICY_NEURAL = 2 };
+/* src/network/activation.rs */
+enum { RLO_ACT_LINEAR = 0, RLO_ACT_TANH = 1, RLO_ACT_RELU = 2, RLO_ACT_LEAKY_RELU = 3, RLO_ACT_RELU6 = 4,
+       RLO_ACT_LEAKY_RELU6 = 5, RLO_ACT_SIGMOID = 6, RLO_ACT_SOFTMAX = 7, RLO_ACT_SWISH = 8,
+       RLO_ACT_HARD_SWISH = 9 };
+enum { RLO_INPUT_SCALAR = 0, RLO_INPUT_FL_OBS = 1 };
 enum { RLO_SEL_EPS_GREEDY = 0, RLO_SEL_UCB = 1 };
 enum { RLO_ALGO_SARSA = 0, RLO_ALGO_QLEARNING = 1, RLO_ALGO_EXPECTED_SARSA = 2 };
 enum { RLO_DECAY_LINEAR = 0, RLO_DECAY_MUL = 1 };
@@ -58,6 +64,11 @@ typedef struct {
     uint64_t lane_offset;     /* global id of local lane 0 (multi-GPU sharding) */
     uint32_t n_lanes, group_size, sync_every;
     uint32_t eval_episodes;   /* episodes per in-train evaluate() call (reference: 100) */
+    /* NeuralPolicy (policy == RLO_POLICY_NEURAL): DenseLayer(n_in, hidden) -> act1 ->
+     * DenseLayer(hidden, A) -> act2, mse loss (src/bin/frozen_lake_neural.rs:130-134) */
+    int32_t net_input;        /* RLO_INPUT_* */
+    uint32_t net_hidden;
+    int32_t net_act1, net_act2;
 } rlo_config;
 
 /* one per-lane-per-step record (same layout as the product's rl_step_record).
@@ -87,6 +98,25 @@ int      rlo_env_start(const rlo_config *c, double *start);   /* initial-state d
 int      rlo_env_walk(const rlo_config *c, uint64_t lane, uint32_t n, const uint32_t *actions,
                       uint32_t *s0, uint32_t *s_next, double *reward, uint8_t *term);
 
+/* fdlibm e_exp / s_expm1 / s_tanh operation sequences (shared with the device) */
+double   rlo_exp(double x);
+double   rlo_expm1(double x);
+double   rlo_tanh(double x);
+/* activation f(x), f'(x) (src/network/activation.rs); not RLO_ACT_SOFTMAX */
+void     rlo_act(int32_t act, double x, double *f, double *fprime);
+/* network sizes for a config: input features and per-agent parameter count
+ * ([W1 n_in x H][b1 H][W2 H x A][b2 A]); -1 if the config has no valid network */
+int      rlo_net_dims(const rlo_config *c, uint32_t *n_in, uint32_t *n_params);
+/* input-adapter features of every dense state, [S][n_in] */
+int      rlo_net_features(const rlo_config *c, double *out);
+/* DenseLayer::new (gen 0: bias 0) / DenseLayer::reset (gen >= 1: bias 0.1) weights of
+ * the agent on lane `lane` (layers.rs:59-73, :90-95) */
+void     rlo_net_init(const rlo_config *c, uint64_t lane, uint32_t gen, double *w);
+/* Network::predict (src/network.rs:51-58): y = act2(W2' act1(W1' x + b1) + b2) */
+void     rlo_net_forward(const rlo_config *c, const double *w, const double *x, double *y);
+/* Network::fit (src/network.rs:61-80), one sample, plain SGD at rate lr */
+void     rlo_net_fit(const rlo_config *c, double *w, const double *x, const double *y_target, double lr);
+
 /* rand 0.8.5 gen_range(0..range) for usize (sample_single_inclusive): index + reject flag */
 uint64_t rlo_gen_index_u64(uint64_t v, uint64_t range, int *reject);
 
@@ -108,6 +138,9 @@ void   rlo_faithful_histories(const rlo_faithful *f, double *reward_history,
 uint64_t rlo_faithful_get_records(const rlo_faithful *f, rlo_record *out, uint64_t cap);
 void   rlo_faithful_set_record(rlo_faithful *f, int enable);
 double rlo_faithful_epsilon(const rlo_faithful *f);
+/* NeuralPolicy parameters (n_params doubles) */
+void   rlo_faithful_get_weights(const rlo_faithful *f, double *out);
+void   rlo_faithful_set_weights(rlo_faithful *f, const double *in);
 /* InternalModelAgent::new(agent, RandomModel::default(), planning_steps)
  * (src/agent/internal_model_agent.rs:20-31); 0 = the plain agent */
 void   rlo_faithful_set_planning(rlo_faithful *f, uint32_t planning_steps);
@@ -132,7 +165,8 @@ void   rlo_batch_run(rlo_batch *b, uint32_t n_launches);
 uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n_episodes, uint64_t eval_at);
 uint64_t rlo_batch_evaluate(rlo_batch *b, uint64_t n_episodes);
 void   rlo_batch_reset(rlo_batch *b);
-/* shared mode (G >= 2): [P][S][A] merged base; private mode (G == 1): [L][P][S][A] f64 */
+/* shared mode (G >= 2): [P][S][A] merged base; private mode (G == 1): [L][P][S][A] f64
+ * (NeuralPolicy: Policy::get_values of every state, [L][1][S][A]) */
 void   rlo_batch_get_q(const rlo_batch *b, double *out);
 void   rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out);   /* P*S*A raw fixed point */
 void   rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out);
@@ -143,6 +177,9 @@ uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap);
 uint64_t rlo_batch_n_records(const rlo_batch *b);
 void   rlo_batch_stats(const rlo_batch *b, uint64_t *out8);
 void   rlo_batch_lane_eps(const rlo_batch *b, double *out);
+/* NeuralPolicy parameters of every lane, [L][n_params] */
+void   rlo_batch_get_weights(const rlo_batch *b, double *out);
+void   rlo_batch_set_weights(rlo_batch *b, const double *in);
 void   rlo_batch_set_selector(rlo_batch *b, int32_t selector);
 void   rlo_batch_set_algo(rlo_batch *b, int32_t algo);
 /* Dyna planning steps per update (private mode only; -1 otherwise) */

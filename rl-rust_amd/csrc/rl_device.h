@@ -158,6 +158,190 @@ __device__ inline double rl_log(double x) {
     return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
+// ------------------------------------------------------------------ exp / expm1 / tanh
+// fdlibm e_exp.c / s_expm1.c / s_tanh.c operation sequences, evaluated
+// identically by the oracle (oracle/rlref.c rlo_exp / rlo_expm1 / rlo_tanh):
+// the neural policy's activations (src/network/activation.rs) agree bit for bit.
+__device__ __forceinline__ uint32_t hi_word(double x) { return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ uint32_t lo_word(double x) { return (uint32_t)(uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double with_hi(double x, uint32_t hi) {
+    const uint64_t u = ((uint64_t)hi << 32) | ((uint64_t)__double_as_longlong(x) & 0xffffffffull);
+    return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ double add_exponent(double y, int k) { return with_hi(y, (uint32_t)((int32_t)hi_word(y) + k * (1 << 20))); }
+
+__device__ inline double rl_exp(double x) {
+    const double huge = 1.0e+300, twom1000 = 9.33263618503218878990e-302,
+                 o_threshold = 7.09782712893383973096e+02, u_threshold = -7.45133219101941108420e+02,
+                 ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00, P1 = 1.66666666666666019037e-01,
+                 P2 = -2.77777777770155933842e-03, P3 = 6.61375632143793436117e-05,
+                 P4 = -1.65339022054652515390e-06, P5 = 4.13813679705723846039e-08;
+    double y, hi = 0.0, lo = 0.0, c, t;
+    int k = 0;
+    uint32_t hx = hi_word(x);
+    const int xsb = (int)((hx >> 31) & 1u);
+    hx &= 0x7fffffffu;
+    if (hx >= 0x40862E42u) {
+        if (hx >= 0x7ff00000u) {
+            if (((hx & 0xfffffu) | lo_word(x)) != 0) return x + x;
+            return xsb == 0 ? x : 0.0;
+        }
+        if (x > o_threshold) return huge * huge;
+        if (x < u_threshold) return twom1000 * twom1000;
+    }
+    if (hx > 0x3fd62e42u) {
+        if (hx < 0x3FF0A2B2u) {
+            hi = x - (xsb ? -ln2HI : ln2HI); lo = xsb ? -ln2LO : ln2LO; k = 1 - xsb - xsb;
+        } else {
+            k = (int)(invln2 * x + (xsb ? -0.5 : 0.5));
+            t = (double)k;
+            hi = x - t * ln2HI;
+            lo = t * ln2LO;
+        }
+        x = hi - lo;
+    } else if (hx < 0x3e300000u) {
+        if (huge + x > 1.0) return 1.0 + x;
+    } else {
+        k = 0;
+    }
+    t = x * x;
+    c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return add_exponent(y, k);
+    return add_exponent(y, k + 1000) * twom1000;
+}
+
+__device__ inline double rl_expm1(double x) {
+    const double huge = 1.0e+300, tiny = 1.0e-300, o_threshold = 7.09782712893383973096e+02,
+                 ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 invln2 = 1.44269504088896338700e+00, Q1 = -3.33333333333331316428e-02,
+                 Q2 = 1.58730158725481460165e-03, Q3 = -7.93650757867487942473e-05,
+                 Q4 = 4.00821782732936239552e-06, Q5 = -2.01099218183624371326e-07;
+    double y, hi, lo, c = 0.0, t, e, hxs, hfx, r1;
+    int k;
+    uint32_t hx = hi_word(x);
+    const uint32_t xsb = hx & 0x80000000u;
+    hx &= 0x7fffffffu;
+    if (hx >= 0x4043687Au) {
+        if (hx >= 0x40862E42u) {
+            if (hx >= 0x7ff00000u) {
+                if (((hx & 0xfffffu) | lo_word(x)) != 0) return x + x;
+                return xsb == 0 ? x : -1.0;
+            }
+            if (x > o_threshold) return huge * huge;
+        }
+        if (xsb != 0) {
+            if (x + tiny < 0.0) return tiny - 1.0;
+        }
+    }
+    if (hx > 0x3fd62e42u) {
+        if (hx < 0x3FF0A2B2u) {
+            if (xsb == 0) { hi = x - ln2_hi; lo = ln2_lo; k = 1; }
+            else { hi = x + ln2_hi; lo = -ln2_lo; k = -1; }
+        } else {
+            k = (int)(invln2 * x + ((xsb == 0) ? 0.5 : -0.5));
+            t = (double)k;
+            hi = x - t * ln2_hi;
+            lo = t * ln2_lo;
+        }
+        x = hi - lo;
+        c = (hi - x) - lo;
+    } else if (hx < 0x3c900000u) {
+        t = huge + x;
+        return x - (t - (huge + x));
+    } else {
+        k = 0;
+    }
+    hfx = 0.5 * x;
+    hxs = x * hfx;
+    r1 = 1.0 + hxs * (Q1 + hxs * (Q2 + hxs * (Q3 + hxs * (Q4 + hxs * Q5))));
+    t = 3.0 - r1 * hfx;
+    e = hxs * ((r1 - t) / (6.0 - x * t));
+    if (k == 0) return x - (x * e - hxs);
+    e = (x * (e - c) - c);
+    e -= hxs;
+    if (k == -1) return 0.5 * (x - e) - 0.5;
+    if (k == 1) {
+        if (x < -0.25) return -2.0 * (e - (x + 0.5));
+        return 1.0 + 2.0 * (x - e);
+    }
+    if (k <= -2 || k > 56) {
+        y = 1.0 - (e - x);
+        y = add_exponent(y, k);
+        return y - 1.0;
+    }
+    if (k < 20) {
+        t = with_hi(0.0, 0x3ff00000u - (0x200000u >> k));
+        y = t - (e - x);
+        y = add_exponent(y, k);
+    } else {
+        t = with_hi(0.0, (uint32_t)((0x3ff - k) << 20));
+        y = x - (e + t);
+        y += 1.0;
+        y = add_exponent(y, k);
+    }
+    return y;
+}
+
+__device__ inline double rl_tanh(double x) {
+    const double tiny = 1.0e-300;
+    double t, z;
+    const int32_t jx = (int32_t)hi_word(x);
+    const int32_t ix = jx & 0x7fffffff;
+    if (ix >= 0x7ff00000) {
+        if (jx >= 0) return 1.0 / x + 1.0;
+        return 1.0 / x - 1.0;
+    }
+    if (ix < 0x40360000) {
+        if (ix < 0x3c800000) return x * (1.0 + x);
+        if (ix >= 0x3ff00000) {
+            t = rl_expm1(2.0 * __builtin_fabs(x));
+            z = 1.0 - 2.0 / (t + 2.0);
+        } else {
+            t = rl_expm1(-2.0 * __builtin_fabs(x));
+            z = -t / (t + 2.0);
+        }
+    } else {
+        z = 1.0 - tiny;
+    }
+    return jx >= 0 ? z : -z;
+}
+
+// ------------------------------------------------------------------ activations
+// src/network/activation.rs (f, f') pairs; f64::max / f64::min return the
+// non-NaN operand.  Softmax (layer-wide) lives in the network code.
+__device__ __forceinline__ double max_rs(double a, double b) { return (a > b || b != b) ? a : b; }
+__device__ __forceinline__ double min_rs(double a, double b) { return (a < b || b != b) ? a : b; }
+__device__ __forceinline__ double sigmoid_(double v) { return 1.0 / (1.0 + rl_exp(-v)); }
+__device__ inline double act_f(int act, double v) {
+    switch (act) {
+    case RL_ACT_TANH: return rl_tanh(v);
+    case RL_ACT_RELU: return max_rs(v, 0.0);
+    case RL_ACT_LEAKY_RELU: return max_rs(v, 0.1 * v);
+    case RL_ACT_RELU6: return min_rs(max_rs(v, 0.0), 6.0);
+    case RL_ACT_LEAKY_RELU6: return min_rs(max_rs(v, 0.1 * v), 6.0);
+    case RL_ACT_SIGMOID: return sigmoid_(v);
+    case RL_ACT_SWISH: return v * sigmoid_(v);
+    case RL_ACT_HARD_SWISH: return (v * min_rs(max_rs(v + 3.0, 0.0), 6.0)) / 6.0;
+    default: return v;
+    }
+}
+__device__ inline double act_fp(int act, double v) {
+    switch (act) {
+    case RL_ACT_TANH: { const double t = rl_tanh(v); return 1.0 - t * t; }
+    case RL_ACT_RELU: return v > 0.0 ? 1.0 : 0.0;
+    case RL_ACT_LEAKY_RELU: return v > 0.0 ? 1.0 : 0.01;
+    case RL_ACT_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.0;
+    case RL_ACT_LEAKY_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.01;
+    case RL_ACT_SIGMOID: { const double sg = sigmoid_(v); return sg * (1.0 - sg); }
+    case RL_ACT_SWISH: { const double e = rl_exp(v); return (e * (v + e + 1.0)) / ((e + 1.0) * (e + 1.0)); }
+    case RL_ACT_HARD_SWISH: return v > -3.0 ? (2.0 * v + 3.0) / 6.0 : 0.0;
+    default: return 1.0;
+    }
+}
+
 // UCB value u_i = q_i + c * sqrt(ln(t) / (n_i + MIN_POSITIVE))
 // (upper_confidence_bound.rs:33-37,53-57); sqrt and / are correctly rounded.
 __device__ __forceinline__ double ucb_value(double q, double c, double lnt, double n) {
@@ -297,6 +481,39 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
         const uint32_t o = (w >> (8 * i)) & 0xffu;
         s2 = o & 63u;
         rew = (o & 64u) ? 1.0 : 0.0;
+        term = (o & 128u) != 0;
+        pos = s2;
+    }
+};
+
+// FrozenLakeEditedEnv (src/env/frozen_lake_edited.rs), dense obs = position.
+// trans[s*4+a] as FrozenLake's: 3 outcome bytes (bits 0-5 next, bit 6 reward
+// 10.0 (else -1.0), bit 7 terminated) + bit 24 "slippery row".  Truncation
+// observes the current position with -1.0 (:227-231); one draw per step (:235).
+template <> struct EnvDev<RL_ENV_FROZEN_LAKE_EDITED> {
+    static constexpr int A = 4;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
+        const double u = uniform01(r);                 // :222-223
+        z = 0;
+        return start_state(t, u);
+    }
+    __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
+                                                const EnvTables &t, uint32_t &s2, double &rew,
+                                                bool &term) {
+        if (z >= t.max_steps) { s2 = pos; rew = -1.0; term = true; return; }
+        z += 1;
+        const uint32_t w = t.trans[pos * 4 + a];
+        uint32_t i = 0;
+        if (t.slippery) {
+            const double u = uniform01(r);
+            if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
+        } else {
+            r.skip_u32();
+            r.skip_u32();
+        }
+        const uint32_t o = (w >> (8 * i)) & 0xffu;
+        s2 = o & 63u;
+        rew = (o & 64u) ? 10.0 : -1.0;
         term = (o & 128u) != 0;
         pos = s2;
     }

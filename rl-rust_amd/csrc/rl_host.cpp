@@ -46,6 +46,8 @@ struct EnvHost {
     double th1 = 0, th2 = 0, th3 = 0, trunc_reward = 0;
     int32_t fixed_start = -1;     // categorical_sample over `cdf` is constant (single start state)
     int32_t slippery = 0;         // FrozenLake with stochastic rows
+    const char *const *map = nullptr;   // FrozenLake / FrozenLakeEdited grid (n x n)
+    int n = 0;
 };
 
 const char *const kFL4[] = {"SFFF", "FHFH", "FFFH", "HFFG"};                     // frozen_lake.rs:23
@@ -66,6 +68,25 @@ void grid_move(int nrow, int ncol, int row, int col, int a, int &nr, int &nc) {
     case 3: nr = std::max(row - 1, 0); break;
     default: break;
     }
+}
+
+// FrozenLakeTerrain of a cell / of the neighbour in direction a, WALL off the
+// grid (src/env/frozen_lake_edited.rs get_obs :115-144, get_terrain :146-162)
+enum { kStart = 0, kWall = 1, kHole = 2, kGround = 3, kGoal = 4 };
+int terrain(const char *const *map, int row, int col) {
+    const char ch = map[row][col];
+    return ch == 'S' ? kStart : ch == 'G' ? kGoal : ch == 'H' ? kHole : kGround;
+}
+int neighbour(const char *const *map, int n, int row, int col, int a) {
+    switch (a) {
+    case 0: return col == 0 ? kWall : terrain(map, row, col - 1);
+    case 1: return row == n - 1 ? kWall : terrain(map, row + 1, col);
+    case 2: return col == n - 1 ? kWall : terrain(map, row, col + 1);
+    default: return row == 0 ? kWall : terrain(map, row - 1, col);
+    }
+}
+double terrain_value(int t) {   // FrozenLakeTerrain::value (frozen_lake_edited.rs:18-28)
+    return t == kHole ? -1.0 : t == kWall ? -0.5 : t == kStart ? 0.0 : t == kGround ? 0.5 : 1.0;
 }
 
 void finish_cdf(EnvHost &e) {
@@ -89,9 +110,12 @@ int build_env(const rl_env_config &c, EnvHost &e) {
     e = EnvHost();
     e.kind = c.kind;
     e.max_steps = c.max_steps;
-    if (c.kind == RL_ENV_FROZEN_LAKE) {
+    if (c.kind == RL_ENV_FROZEN_LAKE || c.kind == RL_ENV_FROZEN_LAKE_EDITED) {
         const char *const *map = c.map8x8 ? kFL8 : kFL4;
         const int n = c.map8x8 ? 8 : 4;
+        const bool edited = c.kind == RL_ENV_FROZEN_LAKE_EDITED;
+        e.map = map;
+        e.n = n;
         e.S = n * n;
         e.A = 4;
         e.trans.assign(e.S * 4, 0);
@@ -103,6 +127,11 @@ int build_env(const rl_env_config &c, EnvHost &e) {
         auto outcome = [&](int row, int col, int a) -> uint32_t {
             int nr, nc;
             grid_move(n, n, row, col, a, nr, nc);
+            if (edited) {   // update_probability_matrix (frozen_lake_edited.rs:94-113): judged by
+                            // the terrain in the moved direction; 10.0 onto G, else -1.0
+                const int t = neighbour(map, n, row, col, a);
+                return (uint32_t)(nr * n + nc) | (t == kGoal ? 64u : 0u) | ((t == kGoal || t == kHole) ? 128u : 0u);
+            }
             const char ch = map[nr][nc];
             return (uint32_t)(nr * n + nc) | (ch == 'G' ? 64u : 0u) | ((ch == 'G' || ch == 'H') ? 128u : 0u);
         };
@@ -124,7 +153,7 @@ int build_env(const rl_env_config &c, EnvHost &e) {
         e.th1 = 0.0 + third;
         e.th2 = e.th1 + third;
         e.th3 = e.th2 + third;
-        e.trunc_reward = 0.0;
+        e.trunc_reward = edited ? -1.0 : 0.0;   // frozen_lake.rs:119-122 / frozen_lake_edited.rs:227-231
     } else if (c.kind == RL_ENV_CLIFF_WALKING) {
         e.S = 48;
         e.A = 4;
@@ -184,6 +213,42 @@ int build_env(const rl_env_config &c, EnvHost &e) {
     }
     if (!e.start.empty()) finish_cdf(e);
     return RL_OK;
+}
+
+// NeuralPolicy input features of every dense state (rl.h rl_input_adapter)
+int net_feature_table(const rl_env_config &c, const EnvHost &e, int input, std::vector<double> &feat, uint32_t &n_in) {
+    if (input == RL_INPUT_FL_OBS) {
+        if (!e.map) return fail(RL_E_ARG, "the FrozenLakeObs adapter needs FrozenLake / FrozenLakeEdited");
+        n_in = 6;
+        feat.assign((size_t)e.S * 6, 0.0);
+        for (uint32_t s = 0; s < e.S; ++s) {
+            const int row = (int)s / e.n, col = (int)s % e.n;
+            for (int a = 0; a < 4; ++a) feat[s * 6 + a] = terrain_value(neighbour(e.map, e.n, row, col, a));
+            feat[s * 6 + 4] = (double)row;
+            feat[s * 6 + 5] = (double)col;
+        }
+        return RL_OK;
+    }
+    if (input != RL_INPUT_SCALAR) return fail(RL_E_ARG, "unknown input adapter");
+    if (c.kind == RL_ENV_FROZEN_LAKE_EDITED)
+        return fail(RL_E_ARG, "FrozenLakeEdited observations are FrozenLakeObs structs: use RL_INPUT_FL_OBS");
+    n_in = 1;
+    feat.assign(e.S, 0.0);
+    for (uint32_t s = 0; s < e.S; ++s) feat[s] = (double)rl_obs_to_reference(c.kind, s);   // obs as f64
+    return RL_OK;
+}
+// rand 0.8.5 UniformFloat::<f64>::new(low, high): scale decreased until
+// scale * max_rand + low < high
+double uniform_scale(double low, double high) {
+    const double max_rand = 1.0 - 0x1p-52;
+    double scale = high - low;
+    while (scale * max_rand + low >= high) {
+        uint64_t b;
+        std::memcpy(&b, &scale, 8);
+        b -= 1;
+        std::memcpy(&scale, &b, 8);
+    }
+    return scale;
 }
 
 // value of a fixed-point Q entry (matches rlamd::q_val on the device)
@@ -267,6 +332,10 @@ struct rl_agent {
     uint32_t plan = 0;
     uint32_t *mcnt = nullptr, *mkey = nullptr, *ms2 = nullptr, *mslot = nullptr;
     double *mr = nullptr;
+    // NeuralPolicy
+    bool neural = false;
+    uint32_t n_in = 0, n_params = 0, net_gen = 0xffffffffu;
+    double *net_w = nullptr, *feat = nullptr;
     // env tables
     uint32_t *trans = nullptr;
     double *cdf = nullptr;
@@ -311,7 +380,15 @@ int agent_select_kernel(rl_agent *a) {
 
 int agent_reset_policy(rl_agent *a) {
     const size_t PSA = (size_t)a->P * a->S * a->A, SA = (size_t)a->S * a->A;
-    if (a->priv) {
+    if (a->neural) {   // NeuralPolicy::new (generation 0) / Network::reset (src/network.rs:89-93)
+        ++a->net_gen;
+        const double l1 = std::sqrt(6.0 / (double)(a->n_in + a->cfg.net.hidden));
+        const double l2 = std::sqrt(6.0 / (double)(a->cfg.net.hidden + a->A));
+        launch_net_init(a->kp, a->cfg.seed, a->cfg.lane_offset, a->net_gen, uniform_scale(-l1, l1), -l1,
+                        uniform_scale(-l2, l2), -l2, a->stream);
+        HIPC(hipGetLastError());
+        HIPC(hipStreamSynchronize(a->stream));
+    } else if (a->priv) {
         launch_fill_f64(a->q_priv, PSA * a->L, a->cfg.q_default, a->stream);
         HIPC(hipGetLastError());
         if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 4, a->stream));
@@ -497,15 +574,18 @@ int rl_env_table(const rl_env_config *cfg, double *prob, uint32_t *next, double 
             uint32_t nx[3] = {0, 0, 0};
             double rw[3] = {0.0, 0.0, 0.0};
             uint8_t tm[3] = {0, 0, 0};
-            if (e.kind == RL_ENV_FROZEN_LAKE) {
+            if (e.kind == RL_ENV_FROZEN_LAKE || e.kind == RL_ENV_FROZEN_LAKE_EDITED) {
+                const bool edited = e.kind == RL_ENV_FROZEN_LAKE_EDITED;
+                const char cell = e.map[s / e.n][s % e.n];
                 const int n = (w >> 24) & 1 ? 3 : 1;
                 for (int i = 0; i < n; ++i) {
                     const uint32_t o = (w >> (8 * i)) & 0xffu;
                     pr[i] = n == 3 ? 1.0 / 3.0 : 1.0;
                     nx[i] = o & 63u;
-                    rw[i] = (o & 64u) ? 1.0 : 0.0;
+                    rw[i] = edited ? ((o & 64u) ? 10.0 : -1.0) : ((o & 64u) ? 1.0 : 0.0);
                     tm[i] = (o & 128u) ? 1 : 0;
                 }
+                if (cell == 'G' || cell == 'H') rw[0] = 0.0;   // (1.0, s, 0.0, true) rows: never stepped from
             } else if (e.kind == RL_ENV_CLIFF_WALKING) {
                 nx[0] = w & 63u;
                 rw[0] = (w & 64u) ? -100.0 : -1.0;
@@ -625,9 +705,16 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     const rl_agent_config &c = *cfg;
     if (c.n_lanes == 0 || c.group_size == 0 || c.group_size > 1024 || c.sync_every == 0)
         return fail(RL_E_ARG, "need n_lanes >= 1, 1 <= group_size <= 1024, sync_every >= 1");
-    if (c.agent < 0 || c.agent > 1 || c.policy < 0 || c.policy > 1 || c.selector < 0 || c.selector > 1 ||
+    if (c.agent < 0 || c.agent > 1 || c.policy < 0 || c.policy > 2 || c.selector < 0 || c.selector > 1 ||
         c.algo < 0 || c.algo > 2 || c.decay_kind < 0 || c.decay_kind > 1)
         return fail(RL_E_ARG, "enum out of range");
+    if (c.policy == RL_POLICY_NEURAL) {
+        if (c.group_size != 1) return fail(RL_E_ARG, "NeuralPolicy runs private agents only (group_size 1)");
+        if (c.net.hidden == 0 || c.net.hidden > RL_NET_MAX_HIDDEN) return fail(RL_E_ARG, "network hidden size out of range");
+        if (c.net.act_hidden < 0 || c.net.act_hidden > RL_ACT_HARD_SWISH || c.net.act_hidden == RL_ACT_SOFTMAX ||
+            c.net.act_out < 0 || c.net.act_out > RL_ACT_HARD_SWISH)
+            return fail(RL_E_ARG, "activation out of range (softmax: output layer only)");
+    }
     rl_agent *a = new rl_agent();
     a->cfg = c;
     int rc = build_env(c.env, a->eh);
@@ -646,8 +733,17 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
         (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, 8 * STATS_REP)) ||
         (rc = dalloc(&a->trans, a->eh.trans.size())) || (rc = dalloc(&a->cdf, a->eh.cdf.size())))
         return bad(rc);
+    a->neural = c.policy == RL_POLICY_NEURAL;
+    if (a->neural) {
+        std::vector<double> feat;
+        if ((rc = net_feature_table(c.env, a->eh, c.net.input, feat, a->n_in))) return bad(rc);
+        a->n_params = a->n_in * c.net.hidden + c.net.hidden + c.net.hidden * a->A + a->A;
+        if ((rc = dalloc(&a->net_w, (size_t)a->n_params * L)) || (rc = dalloc(&a->feat, feat.size()))) return bad(rc);
+        if (hipMemcpy(a->feat, feat.data(), feat.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            return bad(fail(RL_E_HIP, "feature upload"));
+    }
     if (a->priv) {
-        if ((rc = dalloc(&a->q_priv, PSA * L))) return bad(rc);
+        if (!a->neural && (rc = dalloc(&a->q_priv, PSA * L))) return bad(rc);
         // UCB counters are allocated even for eps-greedy: set_action_selector may switch
         if ((rc = dalloc(&a->n_priv, SA * L)) || (rc = dalloc(&a->t_priv, L))) return bad(rc);
     } else {
@@ -690,6 +786,8 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.n_rep = a->n_rep;
     p.delta_words = (uint32_t)a->delta_words;
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
+    p.net_w = a->net_w; p.feat = a->feat; p.n_in = a->n_in; p.n_hidden = c.net.hidden; p.n_params = a->n_params;
+    p.act1 = c.net.act_hidden; p.act2 = c.net.act_out;
     p.trace = a->trace; p.tlist = a->tlist; p.slot_of = a->slot_of; p.tcnt = a->tcnt;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
     p.fixed_start = a->eh.fixed_start;
@@ -721,6 +819,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
+    dfree(a->net_w); dfree(a->feat);
     if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
     delete a;
 }
@@ -854,6 +953,18 @@ int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
     if (!a || !out) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
     const size_t PSA = (size_t)a->P * a->S * a->A;
+    if (a->neural) {   // Policy::get_values of every state: [n_lanes][S][A]
+        if (n < PSA * a->L) return fail(RL_E_ARG, "output too small: need n_lanes*S*A");
+        double *d = nullptr;
+        HIPC(hipMalloc(&d, PSA * a->L * 8));
+        launch_net_values(a->kp, d, a->stream);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(out, d, PSA * a->L * 8, hipMemcpyDeviceToHost, a->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
+        (void)hipFree(d);
+        HIPC(e);
+        return RL_OK;
+    }
     if (a->priv) {
         if (n < PSA * a->L) return fail(RL_E_ARG, "output too small: need n_lanes*P*S*A");
         std::vector<double> tmp(PSA * a->L);
@@ -875,6 +986,7 @@ int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
 
 int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
     if (!a || !in) return fail(RL_E_ARG, "null argument");
+    if (a->neural) return fail(RL_E_STATE, "NeuralPolicy has no table: use rl_agent_set_weights");
     HIPC(hipSetDevice(a->device));
     const size_t PSA = (size_t)a->P * a->S * a->A;
     if (a->priv) {
@@ -1134,6 +1246,78 @@ int rl_kat_ucb(int32_t device, const double *q, const double *nc, const uint64_t
     HIPC(hipGetLastError());
     HIPC(hipMemcpy(out, dy, n * 8ull, hipMemcpyDeviceToHost));
     (void)hipFree(dq); (void)hipFree(dn); (void)hipFree(dy); (void)hipFree(dt);
+    return RL_OK;
+}
+
+}  // extern "C"
+
+// ====================================================================== NeuralPolicy
+extern "C" {
+
+int rl_agent_net_dims(rl_agent *a, uint32_t *n_in, uint32_t *hidden, uint32_t *n_params) {
+    if (!a || !n_in || !hidden || !n_params) return fail(RL_E_ARG, "null argument");
+    if (!a->neural) return fail(RL_E_STATE, "not a NeuralPolicy agent");
+    *n_in = a->n_in;
+    *hidden = a->cfg.net.hidden;
+    *n_params = a->n_params;
+    return RL_OK;
+}
+
+int rl_agent_get_weights(rl_agent *a, double *out, size_t n) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    if (!a->neural) return fail(RL_E_STATE, "not a NeuralPolicy agent");
+    const size_t np = a->n_params, L = a->L;
+    if (n < np * L) return fail(RL_E_ARG, "output too small: need n_lanes*n_params");
+    HIPC(hipSetDevice(a->device));
+    std::vector<double> tmp(np * L);
+    HIPC(hipMemcpyAsync(tmp.data(), a->net_w, tmp.size() * 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (size_t k = 0; k < np; ++k)
+        for (size_t l = 0; l < L; ++l) out[l * np + k] = tmp[k * L + l];
+    return RL_OK;
+}
+
+int rl_agent_set_weights(rl_agent *a, const double *in, size_t n) {
+    if (!a || !in) return fail(RL_E_ARG, "null argument");
+    if (!a->neural) return fail(RL_E_STATE, "not a NeuralPolicy agent");
+    const size_t np = a->n_params, L = a->L;
+    if (n < np * L) return fail(RL_E_ARG, "input too small: need n_lanes*n_params");
+    HIPC(hipSetDevice(a->device));
+    std::vector<double> tmp(np * L);
+    for (size_t k = 0; k < np; ++k)
+        for (size_t l = 0; l < L; ++l) tmp[k * L + l] = in[l * np + k];
+    HIPC(hipMemcpyAsync(a->net_w, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_net_features(const rl_env_config *env, int32_t input, double *out, size_t n) {
+    if (!env || !out) return fail(RL_E_ARG, "null argument");
+    EnvHost e;
+    int rc = build_env(*env, e);
+    if (rc) return rc;
+    std::vector<double> feat;
+    uint32_t n_in = 0;
+    if ((rc = net_feature_table(*env, e, input, feat, n_in))) return rc;
+    if (n < feat.size()) return fail(RL_E_ARG, "output too small: need n_states*n_in");
+    std::memcpy(out, feat.data(), feat.size() * 8);
+    return RL_OK;
+}
+
+int rl_kat_act(int32_t device, int32_t act, const double *x, double *f, double *fp, uint32_t n) {
+    if (!x || !f || !fp) return fail(RL_E_ARG, "null argument");
+    if (act < 0 || act > RL_ACT_HARD_SWISH || act == RL_ACT_SOFTMAX) return fail(RL_E_ARG, "bad activation");
+    HIPC(hipSetDevice(device));
+    double *dx = nullptr, *df = nullptr, *dp = nullptr;
+    HIPC(hipMalloc(&dx, n * 8ull + 8));
+    HIPC(hipMalloc(&df, n * 8ull + 8));
+    HIPC(hipMalloc(&dp, n * 8ull + 8));
+    HIPC(hipMemcpy(dx, x, n * 8ull, hipMemcpyHostToDevice));
+    launch_kat_act(act, dx, df, dp, n, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpy(f, df, n * 8ull, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(fp, dp, n * 8ull, hipMemcpyDeviceToHost));
+    (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dp);
     return RL_OK;
 }
 

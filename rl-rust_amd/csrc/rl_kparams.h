@@ -59,6 +59,12 @@ struct KParams {
     uint32_t *mcnt;        // [L]
     uint32_t *mkey, *ms2, *mslot;   // [S*A][L]
     double *mr;            // [S*A][L]
+    // NeuralPolicy (private mode): per-lane 2-layer MLP, parameters SoA [param][lane]
+    // in the order [W1 n_in x H][b1 H][W2 H x A][b2 A] (rl.h rl_agent_net_dims)
+    double *net_w;         // [n_params][L]
+    const double *feat;    // [S][n_in] input-adapter features
+    uint32_t n_in, n_hidden, n_params;
+    int32_t act1, act2;    // rl_activation of the hidden / output layer
     // env tables
     const uint32_t *trans; // [S][A] packed
     const double *start_cdf;
@@ -109,5 +115,10 @@ void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);
 void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s);
 void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,
                     uint32_t n, hipStream_t s);
+void launch_kat_act(int act, const double *x, double *f, double *fp, uint32_t n, hipStream_t s);
+// NeuralPolicy: DenseLayer::new / reset weights (gen 0 / >= 1) and get_values of every state
+void launch_net_init(const KParams &p, uint64_t seed, uint64_t lane_offset, uint32_t gen, double scale1,
+                     double low1, double scale2, double low2, hipStream_t s);
+void launch_net_values(const KParams &p, double *out, hipStream_t s);
 
 }  // namespace rlamd

@@ -9,6 +9,7 @@ train_launch_fn train_table_frozen_lake(int, int, int, int, int);
 train_launch_fn train_table_cliff_walking(int, int, int, int, int);
 train_launch_fn train_table_taxi(int, int, int, int, int);
 train_launch_fn train_table_blackjack(int, int, int, int, int);
+train_launch_fn train_table_frozen_lake_edited(int, int, int, int, int);
 
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv) {
     switch (env) {
@@ -16,6 +17,7 @@ train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, 
     case RL_ENV_CLIFF_WALKING: return train_table_cliff_walking(agent, policy, sel, algo, priv);
     case RL_ENV_TAXI: return train_table_taxi(agent, policy, sel, algo, priv);
     case RL_ENV_BLACKJACK: return train_table_blackjack(agent, policy, sel, algo, priv);
+    case RL_ENV_FROZEN_LAKE_EDITED: return train_table_frozen_lake_edited(agent, policy, sel, algo, priv);
     }
     return nullptr;
 }
@@ -192,6 +194,7 @@ void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs) {
     case RL_ENV_CLIFF_WALKING: hipLaunchKernelGGL(k_env_reset<RL_ENV_CLIFF_WALKING>, g, b, 0, s, p, obs); break;
     case RL_ENV_TAXI: hipLaunchKernelGGL(k_env_reset<RL_ENV_TAXI>, g, b, 0, s, p, obs); break;
     case RL_ENV_BLACKJACK: hipLaunchKernelGGL(k_env_reset<RL_ENV_BLACKJACK>, g, b, 0, s, p, obs); break;
+    case RL_ENV_FROZEN_LAKE_EDITED: hipLaunchKernelGGL(k_env_reset<RL_ENV_FROZEN_LAKE_EDITED>, g, b, 0, s, p, obs); break;
     }
 }
 void launch_env_step(int env, const KParams &p, hipStream_t s, const uint32_t *act, uint64_t *obs,
@@ -202,10 +205,73 @@ void launch_env_step(int env, const KParams &p, hipStream_t s, const uint32_t *a
     case RL_ENV_CLIFF_WALKING: hipLaunchKernelGGL(k_env_step<RL_ENV_CLIFF_WALKING>, g, b, 0, s, p, act, obs, rew, term); break;
     case RL_ENV_TAXI: hipLaunchKernelGGL(k_env_step<RL_ENV_TAXI>, g, b, 0, s, p, act, obs, rew, term); break;
     case RL_ENV_BLACKJACK: hipLaunchKernelGGL(k_env_step<RL_ENV_BLACKJACK>, g, b, 0, s, p, act, obs, rew, term); break;
+    case RL_ENV_FROZEN_LAKE_EDITED: hipLaunchKernelGGL(k_env_step<RL_ENV_FROZEN_LAKE_EDITED>, g, b, 0, s, p, act, obs, rew, term); break;
+    }
+}
+
+// ---------------------------------------------------------------- NeuralPolicy
+// DenseLayer::new (gen 0) / DenseLayer::reset (gen k >= 1) of every lane's network
+// (src/network/layers.rs:55-73, :90-95): W ~ rand 0.8.5 Uniform::new(-l, l) drawn
+// row-major from the lane's weight stream (seed ^ 0xD1B54A32D192ED03*(gen+1),
+// global lane), value0_1 * scale + low; b = 0 (new) or 0.1 (reset).  The host
+// passes each layer's (scale, low) (UniformFloat::new's scale search).
+__global__ void k_net_init(KParams p, uint64_t seed, uint64_t lane_offset, uint32_t gen, double scale1, double low1,
+                           double scale2, double low2) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    const uint4 r0 = rng_seed(seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(gen + 1u)), lane_offset + lane);
+    Rng r{r0.x, r0.y, r0.z, r0.w};
+    const uint32_t nw1 = p.n_in * p.n_hidden, nw2 = p.n_hidden * p.A;
+    const double bias = gen ? 0.1 : 0.0;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < nw1; ++i, ++k) {
+        const uint64_t bits = (r.next_u64() >> 12) | 0x3FF0000000000000ull;
+        p.net_w[(uint64_t)k * p.L + lane] = (__longlong_as_double((long long)bits) - 1.0) * scale1 + low1;
+    }
+    for (uint32_t i = 0; i < p.n_hidden; ++i, ++k) p.net_w[(uint64_t)k * p.L + lane] = bias;
+    for (uint32_t i = 0; i < nw2; ++i, ++k) {
+        const uint64_t bits = (r.next_u64() >> 12) | 0x3FF0000000000000ull;
+        p.net_w[(uint64_t)k * p.L + lane] = (__longlong_as_double((long long)bits) - 1.0) * scale2 + low2;
+    }
+    for (uint32_t i = 0; i < p.A; ++i, ++k) p.net_w[(uint64_t)k * p.L + lane] = bias;
+}
+void launch_net_init(const KParams &p, uint64_t seed, uint64_t lane_offset, uint32_t gen, double scale1,
+                     double low1, double scale2, double low2, hipStream_t s) {
+    hipLaunchKernelGGL(k_net_init, dim3((p.L + 255) / 256), dim3(256), 0, s, p, seed, lane_offset, gen, scale1, low1,
+                       scale2, low2);
+}
+// Policy::get_values of every state for every lane: out[lane][s][a]
+template <int A>
+__global__ void k_net_values(KParams p, double *out) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    const NetLane n{p.net_w, p.L, lane, p.n_in, p.n_hidden, (uint32_t)A};
+    for (uint32_t st = 0; st < p.S; ++st) {
+        double x[NET_MAX_IN], opre[A], y[A];
+        net_input(p, st, x);
+        net_forward<A>(p, n, x, opre, y);
+#pragma unroll
+        for (int i = 0; i < A; ++i) out[(lane * p.S + st) * A + i] = y[i];
+    }
+}
+void launch_net_values(const KParams &p, double *out, hipStream_t s) {
+    const dim3 g((p.L + 255) / 256), b(256);
+    switch (p.A) {
+    case 2: hipLaunchKernelGGL(k_net_values<2>, g, b, 0, s, p, out); break;
+    case 4: hipLaunchKernelGGL(k_net_values<4>, g, b, 0, s, p, out); break;
+    case 6: hipLaunchKernelGGL(k_net_values<6>, g, b, 0, s, p, out); break;
     }
 }
 
 // ---------------------------------------------------------------- KAT probes
+__global__ void k_kat_act(int act, const double *x, double *f, double *fp, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { f[i] = act_f(act, x[i]); fp[i] = act_fp(act, x[i]); }
+}
+void launch_kat_act(int act, const double *x, double *f, double *fp, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_kat_act, dim3((n + 255) / 256), dim3(256), 0, s, act, x, f, fp, n);
+}
+
 __global__ void k_kat_log(const double *x, double *out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = rl_log(x[i]);

@@ -14,6 +14,7 @@
 //                   reference's arithmetic bit for bit.
 #pragma once
 #include "rl_device.h"
+#include "rl_net.h"
 
 namespace rlamd {
 
@@ -46,7 +47,8 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
     l.rcp = off; off += shared_q ? align16((nthr + 1u) * 8u) : 0u;
     l.tr = off; off += env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
-    l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_TAXI) ? align16(n_start * 8u) : 0u;
+    l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED || env == RL_ENV_TAXI)
+                            ? align16(n_start * 8u) : 0u;
     l.total = off;
     return l;
 }
@@ -306,7 +308,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
     if constexpr (ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
-    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_TAXI)
+    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
         for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
@@ -607,7 +609,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     if (tid < 8) ACC[tid] = 0ull;
     if constexpr (ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
-    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_TAXI)
+    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
         for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
@@ -634,17 +636,45 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
     constexpr int A = E::A;
     constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
     constexpr bool UCB = SEL == RL_SEL_UCB;
+    constexpr bool NEURAL = POLICY == RL_POLICY_NEURAL;
     const uint32_t SA = p.S * (uint32_t)A;
     const uint64_t Ls = p.L;
     uint64_t t = UCB ? p.t_priv[lane] : 0;
     uint32_t tcnt = AGENT == RL_AGENT_TRACES ? p.tcnt[lane] : 0u;
+    const NetLane net{p.net_w, Ls, lane, p.n_in, p.n_hidden, (uint32_t)A};
+    NetCache<A> nc;
 
     auto qref = [&](uint32_t idx) -> double & { return p.q_priv[(uint64_t)idx * Ls + lane]; };
+    // Policy::predict (tabular_policy.rs:27-29, double_tabular_policy.rs:31-40, neural_policy.rs:43-47)
     auto predict = [&](uint32_t s, double (&v)[A]) {
+        if constexpr (NEURAL) {
+            nc.get(p, net, s);
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = nc.y[i];
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < A; ++i) {
             if constexpr (P == 1) v[i] = qref(s * A + i);
             else v[i] = (qref(s * A + i) + qref(SA + s * A + i)) / 2.0;
+        }
+    };
+    // Policy::get_values of table `tbl` (double policy: flag ? alpha : beta)
+    auto values = [&](uint32_t tbl, uint32_t s, double (&v)[A]) {
+        if constexpr (NEURAL) {
+            predict(s, v);
+        } else {
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = qref(tbl * SA + s * A + i);
+        }
+    };
+    // Policy::update with x = td (one-step) or td * E[o][b] (traces)
+    auto pol_update = [&](uint32_t tbl, uint32_t s, uint32_t a, double x) {
+        if constexpr (NEURAL) {
+            net_policy_update<A>(p, net, nc, s, a, x);
+        } else {
+            double &q = qref(tbl * SA + s * A + a);             // tabular_policy.rs:36
+            q = q + p.lr * x;
         }
     };
     // get_action with the reference's immediate UCB increments
@@ -672,8 +702,9 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;
         const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;
         double q2[A], pr[A];
+        values(vt, s2, q2);
 #pragma unroll
-        for (int i = 0; i < A; ++i) { q2[i] = qref(vt * SA + s2 * A + i); pr[i] = 0.0; }
+        for (int i = 0; i < A; ++i) pr[i] = 0.0;
         if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) {
             if constexpr (!UCB) {
                 eps_probs<A>(L.eps, q2, pr);
@@ -690,18 +721,23 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             }
         }
         const double fq = future_q<ALGO, A>(q2, a2, pr);
-        const double qa = qref(vt * SA + s * A + a);
+        double qa;
+        if constexpr (NEURAL) {
+            double qs[A];
+            values(vt, s, qs);
+            qa = pick<A>(qs, a);
+        } else {
+            qa = qref(vt * SA + s * A + a);
+        }
         const double td = r + p.gamma * fq - qa;
         if constexpr (AGENT == RL_AGENT_ONE_STEP) {
-            double &q = qref(ut * SA + s * A + a);             // tabular_policy.rs:36
-            q = q + p.lr * td;
+            pol_update(ut, s, a, td);
         } else {
+            // the sweep runs in first-visit (slot) order: order-free for the
+            // tabular policies, and the oracle's order for the neural one
             trace_visit<A>(p, lane, s, a, tcnt);
             C.trace_states += tcnt;
-            trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) {
-                double &q = qref(ut * SA + o * A + b);
-                q = q + p.lr * (td * ev);
-            });
+            trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) { pol_update(ut, o, b, td * ev); });
             if (term) tcnt = 0;
         }
         if (P == 2) L.dflag = !L.dflag;                        // after_update
@@ -813,6 +849,13 @@ train_launch_fn train_table_entry(int agent, int policy, int sel, int algo, int 
 #define RLAMD_E4(AG) RLAMD_E3(AG, RL_POLICY_TABULAR) RLAMD_E3(AG, RL_POLICY_DOUBLE)
     RLAMD_E4(RL_AGENT_ONE_STEP)
     RLAMD_E4(RL_AGENT_TRACES)
+    // NeuralPolicy: private agents only
+#define RLAMD_N2(AG, SE)                                                                           \
+    RLAMD_E(AG, RL_POLICY_NEURAL, SE, RL_ALGO_SARSA, 1) RLAMD_E(AG, RL_POLICY_NEURAL, SE, RL_ALGO_QLEARNING, 1) \
+    RLAMD_E(AG, RL_POLICY_NEURAL, SE, RL_ALGO_EXPECTED_SARSA, 1)
+    RLAMD_N2(RL_AGENT_ONE_STEP, RL_SEL_EPS_GREEDY) RLAMD_N2(RL_AGENT_ONE_STEP, RL_SEL_UCB)
+    RLAMD_N2(RL_AGENT_TRACES, RL_SEL_EPS_GREEDY) RLAMD_N2(RL_AGENT_TRACES, RL_SEL_UCB)
+#undef RLAMD_N2
 #undef RLAMD_E4
 #undef RLAMD_E3
 #undef RLAMD_E2

@@ -15,9 +15,12 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("RLAMD_LIB", os.path.join(HERE, "lib", "librlamd.so"))
 INCLUDE_H = os.path.join(ROOT, "include", "rl.h")
 
-ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}
+ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3, "frozen_lake_edited": 4}
 AGENT = {"one_step": 0, "traces": 1}
-POLICY = {"tabular": 0, "double": 1}
+POLICY = {"tabular": 0, "double": 1, "neural": 2}
+ACT = {"linear": 0, "tanh": 1, "relu": 2, "leaky_relu": 3, "relu6": 4, "leaky_relu6": 5,
+       "sigmoid": 6, "softmax": 7, "swish": 8, "hard_swish": 9}
+INPUT = {"scalar": 0, "fl_obs": 1}
 SELECTOR = {"eps_greedy": 0, "ucb": 1}
 ALGO = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}
 RL_OK, RL_E_NOT_READY = 0, 1
@@ -34,6 +37,11 @@ class EnvConfig(C.Structure):
                 ("max_steps", C.c_uint32)]
 
 
+class NetConfig(C.Structure):
+    _fields_ = [("input", C.c_int32), ("hidden", C.c_uint32), ("act_hidden", C.c_int32),
+                ("act_out", C.c_int32)]
+
+
 class AgentConfig(C.Structure):
     _fields_ = [
         ("env", EnvConfig),
@@ -45,6 +53,7 @@ class AgentConfig(C.Structure):
         ("seed", C.c_uint64), ("lane_offset", C.c_uint64),
         ("n_lanes", C.c_uint32), ("group_size", C.c_uint32), ("sync_every", C.c_uint32),
         ("eval_episodes", C.c_uint32), ("device", C.c_int32),
+        ("net", NetConfig),
     ]
 
 
@@ -113,6 +122,11 @@ SIGNATURES = {
     "rl_kat_log": (C.c_int, [C.c_int32, _V, _V, C.c_uint32]),
     "rl_kat_rng": (C.c_int, [C.c_int32, C.c_uint64, C.c_uint64, C.c_uint32, _V]),
     "rl_kat_ucb": (C.c_int, [C.c_int32, _V, _V, _V, C.c_double, _V, C.c_uint32]),
+    "rl_kat_act": (C.c_int, [C.c_int32, C.c_int32, _V, _V, _V, C.c_uint32]),
+    "rl_agent_net_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
+    "rl_agent_get_weights": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_set_weights": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_net_features": (C.c_int, [_P(EnvConfig), C.c_int32, _V, C.c_size_t]),
 }
 
 _lib = None
@@ -151,7 +165,8 @@ def default_params(**kw):
              policy="tabular", selector="eps_greedy", algo="qlearning", decay_kind=0,
              lr=0.05, gamma=0.95, lambda_=0.5, eps0=1.0, n_episodes_for_decay=100000,
              exploration_time=0.5, eps_final=0.0, ucb_c=0.5, q_default=0.0, seed=0x5EED,
-             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100, device=0)
+             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100, device=0,
+             net_input="scalar", net_hidden=32, net_act1="leaky_relu6", net_act2="linear")
     p.update(kw)
     if "eps_decay" not in p:
         p["eps_decay"] = p["eps0"] / (p["exploration_time"] * p["n_episodes_for_decay"])
@@ -171,6 +186,10 @@ def agent_config(p):
     c.seed, c.lane_offset = p["seed"], p["lane_offset"]
     c.n_lanes, c.group_size, c.sync_every = p["n_lanes"], p["group_size"], p["sync_every"]
     c.eval_episodes, c.device = p["eval_episodes"], p["device"]
+    c.net.input = INPUT[p.get("net_input", "scalar")]
+    c.net.hidden = p.get("net_hidden", 32)
+    c.net.act_hidden = ACT[p.get("net_act1", "leaky_relu6")]
+    c.net.act_out = ACT[p.get("net_act2", "linear")]
     return c
 
 
@@ -352,6 +371,22 @@ class Agent:
         check(lib().rl_agent_take_episodes(self.h, out.ctypes.data, n.value, C.byref(n), C.byref(lost)))
         return out, lost.value
 
+    # ---- NeuralPolicy parameters (Layer::get_weights / set_weights)
+    def net_dims(self):
+        n_in, hid, npar = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().rl_agent_net_dims(self.h, C.byref(n_in), C.byref(hid), C.byref(npar)))
+        return n_in.value, hid.value, npar.value
+
+    def weights(self):
+        _, _, npar = self.net_dims()
+        out = np.zeros(self.L * npar, np.float64)
+        check(lib().rl_agent_get_weights(self.h, out.ctypes.data, out.size))
+        return out.reshape(self.L, npar)
+
+    def set_weights(self, w):
+        w = np.ascontiguousarray(w, dtype=np.float64).reshape(-1)
+        check(lib().rl_agent_set_weights(self.h, w.ctypes.data, w.size))
+
     def lane_state(self):
         core = np.zeros((self.L, 4), np.uint32)
         aux = np.zeros((self.L, 4), np.uint32)
@@ -396,6 +431,23 @@ def kat_rng(seed, lane, n, device=0):
     out = np.zeros(n, np.uint32)
     check(lib().rl_kat_rng(device, seed, lane, n, out.ctypes.data))
     return out
+
+
+def kat_act(act, x, device=0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    f, fp = np.zeros_like(x), np.zeros_like(x)
+    check(lib().rl_kat_act(device, ACT[act], x.ctypes.data, f.ctypes.data, fp.ctypes.data, x.size))
+    return f, fp
+
+
+def net_features(p):
+    """input-adapter features of every dense state (no GPU needed)"""
+    S, _ = env_dims(p)
+    c = env_config(p)
+    n_in = 6 if p.get("net_input", "scalar") == "fl_obs" else 1
+    out = np.zeros(S * n_in, np.float64)
+    check(lib().rl_net_features(C.byref(c), INPUT[p.get("net_input", "scalar")], out.ctypes.data, out.size))
+    return out.reshape(S, n_in)
 
 
 def kat_ucb(q, ncount, t, c, device=0):

@@ -4,6 +4,8 @@ and the product's C++ host code), plus hand-derived known answers.
 
 Sources restated (paths in the reference repo):
   FrozenLakeEnv::new      src/env/frozen_lake.rs:23-28 (maps), :30-102
+  FrozenLakeEditedEnv::new src/env/frozen_lake_edited.rs:18-28 (terrain values), :94-218
+  Network::fit            src/network.rs:61-80, src/network/layers.rs:75-141, loss.rs (net_kat)
   CliffWalkingEnv::new    src/env/cliff_walking.rs:9-58
   TaxiEnv::new            src/env/taxi.rs:22-31 (map, locs), :57-131
   utils::inc / from_2d_to_1d / categorical_sample   src/utils.rs:33-76
@@ -60,6 +62,108 @@ def frozen_lake(name, slippery):
     cnt = sum(ch == "S" for r in m for ch in r)
     start = [(1.0 / cnt) if m[i // n][i % n] == "S" else 0.0 for i in range(S)]
     return table, start
+
+
+WALL, HOLE, START, GROUND, GOAL = "WALL", "HOLE", "START", "GROUND", "GOAL"
+TERRAIN_VALUE = {HOLE: -1.0, WALL: -0.5, START: 0.0, GROUND: 0.5, GOAL: 1.0}
+
+
+def fle_terrain(m, row, col):
+    """get_terrain (frozen_lake_edited.rs:146-162); off-map -> WALL"""
+    if row < 0 or col < 0 or row >= len(m) or col >= len(m[0]):
+        return WALL
+    return {"S": START, "F": GROUND, "G": GOAL, "H": HOLE}[m[row][col]]
+
+
+def fle_obs(m, row, col):
+    """get_obs (:115-144): terrains left, down, right, up + (x, y) = (row, col)"""
+    return [fle_terrain(m, row, col - 1), fle_terrain(m, row + 1, col), fle_terrain(m, row, col + 1),
+            fle_terrain(m, row - 1, col), row, col]
+
+
+def frozen_lake_edited(name, slippery):
+    m = FL_MAPS[name]
+    n = len(m)
+    table = []
+    for s in range(n * n):
+        row, col = divmod(s, n)
+        per_a = []
+        for a in range(4):
+            outs = [(0.0, 0, 0.0, False)] * 3
+            if m[row][col] in "GH":
+                outs = [(1.0, s, 0.0, True)] + outs[1:]
+            else:
+                bs = [(a - 1) % 4, a, (a + 1) % 4] if slippery else [a]
+                new = []
+                for b in bs:
+                    nxt = fle_obs(m, row, col)[b]          # terrain in the moved direction
+                    nr, nc = inc(n, n, row, col, b)
+                    win = nxt == GOAL
+                    new.append(((1.0 / 3.0) if slippery else 1.0, nr * n + nc, 10.0 if win else -1.0,
+                                win or nxt == HOLE))
+                outs = new + outs[len(new):]
+            per_a.append(outs)
+        table.append(per_a)
+    cnt = sum(ch == "S" for r in m for ch in r)
+    start = [(1.0 / cnt) if m[i // n][i % n] == "S" else 0.0 for i in range(n * n)]
+    features = [[TERRAIN_VALUE[t] for t in fle_obs(m, *divmod(s, n))[:4]] + [float(s // n), float(s % n)]
+                for s in range(n * n)]
+    return table, start, features
+
+
+def net_kat():
+    """One Network::fit step of the neural bin's shape (DenseLayer(1,H) -> leaky_relu6 ->
+    DenseLayer(H,4) -> linear, mse) on fixed weights, in plain Python floats (IEEE
+    double, no FMA): sums over k in order from 0.0 (ndarray dot), Dense backward
+    input_error with the old W, W -= lr * input^T err, b -= lr * err."""
+    H, A, lr = 3, 4, 0.05
+    W1 = [[0.25, -0.5, 0.125]]
+    b1 = [0.1, -0.2, 0.0]
+    W2 = [[0.5, -0.25, 0.75, 0.1], [-0.3, 0.2, 0.4, -0.6], [0.05, 0.15, -0.35, 0.45]]
+    b2 = [0.0, 0.1, -0.1, 0.2]
+    x = [3.0]
+
+    def lrelu6(v):
+        return min(max(v, 0.1 * v), 6.0)
+
+    def lrelu6p(v):
+        return 1.0 if 0.0 < v < 6.0 else 0.01
+
+    def forward():
+        z = [0.0 + x[0] * W1[0][j] + b1[j] for j in range(H)]
+        h = [lrelu6(v) for v in z]
+        o = []
+        for i in range(A):
+            acc = 0.0
+            for j in range(H):
+                acc = acc + h[j] * W2[j][i]
+            o.append(acc + b2[i])
+        return z, h, o
+
+    z, h, y = forward()
+    target = list(y)
+    target[2] += -0.7                                     # curr_values[action] += td
+    err = [(2.0 * (y[i] - target[i])) / A for i in range(A)]
+    e2 = [1.0 * err[i] for i in range(A)]                 # linear_prime * err
+    ie = []
+    for j in range(H):
+        acc = 0.0
+        for i in range(A):
+            acc = acc + e2[i] * W2[j][i]
+        ie.append(acc)
+    for j in range(H):
+        for i in range(A):
+            W2[j][i] = W2[j][i] - lr * (0.0 + h[j] * e2[i])
+    b2 = [b2[i] - lr * e2[i] for i in range(A)]
+    e1 = [lrelu6p(z[j]) * ie[j] for j in range(H)]
+    for j in range(H):
+        W1[0][j] = W1[0][j] - lr * (0.0 + x[0] * e1[j])
+    b1 = [b1[j] - lr * e1[j] for j in range(H)]
+    flat = lambda W1, b1, W2, b2: [v for r in W1 for v in r] + list(b1) + [v for r in W2 for v in r] + list(b2)
+    w0 = flat([[0.25, -0.5, 0.125]], [0.1, -0.2, 0.0],
+              [[0.5, -0.25, 0.75, 0.1], [-0.3, 0.2, 0.4, -0.6], [0.05, 0.15, -0.35, 0.45]], [0.0, 0.1, -0.1, 0.2])
+    return {"hidden": H, "lr": lr, "x": x, "w": w0, "y": y, "target": target,
+            "w_after": flat(W1, b1, W2, b2)}
 
 
 def cliff_walking():
@@ -153,6 +257,11 @@ def main():
         for slip in (0, 1):
             t, st = frozen_lake(name, slip)
             out[f"frozen_lake_{name}_{'slippery' if slip else 'det'}"] = dict(pack(t), start=st)
+    for name in ("4x4", "8x8"):
+        for slip in (0, 1):
+            t, st, feat = frozen_lake_edited(name, slip)
+            out[f"frozen_lake_edited_{name}_{'slippery' if slip else 'det'}"] = dict(pack(t), start=st,
+                                                                                   fl_obs=feat)
     t, st = cliff_walking()
     out["cliff_walking"] = dict(pack(t), start=st)
     t, st = taxi()
@@ -170,6 +279,7 @@ def main():
         "ucb_first_inf_t": next(t for t in range(2, 200) if __import__("math").log(t) / 2.2250738585072014e-308 == float("inf")),
         "uniform_int_reject_6": (2**64 - 6) % 6,
         "uniform_card_reject": (2**32 - 10) % 10,
+        "net_fit_leaky_relu6": net_kat(),
     }
     out["kat"] = kat
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tables.json")

@@ -13,9 +13,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "_build", "librlref.so")
 
-ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}
+ENV = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3, "frozen_lake_edited": 4}
 AGENT = {"one_step": 0, "traces": 1}
-POLICY = {"tabular": 0, "double": 1}
+POLICY = {"tabular": 0, "double": 1, "neural": 2}
+ACT = {"linear": 0, "tanh": 1, "relu": 2, "leaky_relu": 3, "relu6": 4, "leaky_relu6": 5,
+       "sigmoid": 6, "softmax": 7, "swish": 8, "hard_swish": 9}
+INPUT = {"scalar": 0, "fl_obs": 1}
 SELECTOR = {"eps_greedy": 0, "ucb": 1}
 ALGO = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}
 MODE_TRAIN, MODE_EVAL, MODE_DONE = 0, 1, 2
@@ -33,6 +36,8 @@ class Config(C.Structure):
         ("seed", C.c_uint64), ("lane_offset", C.c_uint64),
         ("n_lanes", C.c_uint32), ("group_size", C.c_uint32), ("sync_every", C.c_uint32),
         ("eval_episodes", C.c_uint32),
+        ("net_input", C.c_int32), ("net_hidden", C.c_uint32),
+        ("net_act1", C.c_int32), ("net_act2", C.c_int32),
     ]
 
 
@@ -49,7 +54,8 @@ def default_params(**kw):
              policy="tabular", selector="eps_greedy", algo="qlearning", decay_kind=0,
              lr=0.05, gamma=0.95, lambda_=0.5, eps0=1.0, n_episodes_for_decay=100000,
              exploration_time=0.5, eps_final=0.0, ucb_c=0.5, q_default=0.0, seed=0x5EED,
-             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100)
+             lane_offset=0, n_lanes=1, group_size=1, sync_every=64, eval_episodes=100,
+             net_input="scalar", net_hidden=32, net_act1="leaky_relu6", net_act2="linear")
     p.update(kw)
     if "eps_decay" not in p:
         p["eps_decay"] = p["eps0"] / (p["exploration_time"] * p["n_episodes_for_decay"])
@@ -70,6 +76,10 @@ def make_config(p):
     c.seed, c.lane_offset = p["seed"], p["lane_offset"]
     c.n_lanes, c.group_size, c.sync_every = p["n_lanes"], p["group_size"], p["sync_every"]
     c.eval_episodes = p["eval_episodes"]
+    c.net_input = INPUT[p.get("net_input", "scalar")]
+    c.net_hidden = p.get("net_hidden", 32)
+    c.net_act1 = ACT[p.get("net_act1", "leaky_relu6")]
+    c.net_act2 = ACT[p.get("net_act2", "linear")]
     return c
 
 
@@ -153,6 +163,18 @@ def lib():
         L.rlo_batch_lane_eps.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_set_selector.argtypes = [C.c_void_p, C.c_int32]
         L.rlo_batch_set_algo.argtypes = [C.c_void_p, C.c_int32]
+        for fn in ("rlo_exp", "rlo_expm1", "rlo_tanh"):
+            getattr(L, fn).restype = C.c_double
+            getattr(L, fn).argtypes = [C.c_double]
+        L.rlo_act.argtypes = [C.c_int32, C.c_double, P(C.c_double), P(C.c_double)]
+        L.rlo_net_dims.argtypes = [P(Config), P(C.c_uint32), P(C.c_uint32)]
+        L.rlo_net_features.argtypes = [P(Config), C.c_void_p]
+        L.rlo_net_init.argtypes = [P(Config), C.c_uint64, C.c_uint32, C.c_void_p]
+        L.rlo_net_forward.argtypes = [P(Config), C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rlo_net_fit.argtypes = [P(Config), C.c_void_p, C.c_void_p, C.c_void_p, C.c_double]
+        for fn in ("rlo_faithful_get_weights", "rlo_faithful_set_weights", "rlo_batch_get_weights",
+                   "rlo_batch_set_weights"):
+            getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -195,6 +217,61 @@ def env_walk(p, actions, lane=0):
                            r.ctypes.data, t.ctypes.data)
     assert k >= 0
     return s0.value, s2[:k], r[:k], t[:k].astype(bool), k
+
+
+def act(name, x):
+    """activation f(x), f'(x) (src/network/activation.rs), elementwise"""
+    x = np.asarray(x, np.float64).reshape(-1)
+    f, fp = np.zeros_like(x), np.zeros_like(x)
+    a, b = C.c_double(), C.c_double()
+    for i, v in enumerate(x):
+        lib().rlo_act(ACT[name], float(v), C.byref(a), C.byref(b))
+        f[i], fp[i] = a.value, b.value
+    return f, fp
+
+
+def net_dims(p):
+    c = make_config(p)
+    n_in, n_par = C.c_uint32(), C.c_uint32()
+    assert lib().rlo_net_dims(C.byref(c), C.byref(n_in), C.byref(n_par)) == 0, "no valid network"
+    return n_in.value, n_par.value
+
+
+def net_features(p):
+    S, _ = dims(p)
+    n_in, _ = net_dims(p)
+    out = np.zeros(S * n_in, np.float64)
+    c = make_config(p)
+    assert lib().rlo_net_features(C.byref(c), out.ctypes.data) == 0
+    return out.reshape(S, n_in)
+
+
+def net_init(p, lane, gen=0):
+    _, n_par = net_dims(p)
+    w = np.zeros(n_par, np.float64)
+    c = make_config(p)
+    lib().rlo_net_init(C.byref(c), lane, gen, w.ctypes.data)
+    return w
+
+
+def net_forward(p, w, x):
+    _, A = dims(p)
+    y = np.zeros(A, np.float64)
+    c = make_config(p)
+    w = np.ascontiguousarray(w, np.float64)
+    x = np.ascontiguousarray(x, np.float64)
+    lib().rlo_net_forward(C.byref(c), w.ctypes.data, x.ctypes.data, y.ctypes.data)
+    return y
+
+
+def net_fit(p, w, x, y, lr):
+    """Network::fit in place on a copy; returns the new parameters"""
+    c = make_config(p)
+    w = np.array(w, np.float64)
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    lib().rlo_net_fit(C.byref(c), w.ctypes.data, x.ctypes.data, y.ctypes.data, float(lr))
+    return w
 
 
 def rng_stream(seed, lane, n):
@@ -256,6 +333,16 @@ class Faithful:
 
     def epsilon(self):
         return lib().rlo_faithful_epsilon(self.h)
+
+    def weights(self):
+        _, n_par = net_dims(self.p)
+        out = np.zeros(n_par, np.float64)
+        lib().rlo_faithful_get_weights(self.h, out.ctypes.data)
+        return out
+
+    def set_weights(self, w):
+        w = np.ascontiguousarray(w, np.float64)
+        lib().rlo_faithful_set_weights(self.h, w.ctypes.data)
 
 
 class Batch:
@@ -360,3 +447,13 @@ class Batch:
         out = np.zeros(self.L, np.float64)
         lib().rlo_batch_lane_eps(self.h, out.ctypes.data)
         return out
+
+    def weights(self):
+        _, n_par = net_dims(self.p)
+        out = np.zeros(self.L * n_par, np.float64)
+        lib().rlo_batch_get_weights(self.h, out.ctypes.data)
+        return out.reshape(self.L, n_par)
+
+    def set_weights(self, w):
+        w = np.ascontiguousarray(w, np.float64)
+        lib().rlo_batch_set_weights(self.h, w.ctypes.data)

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol(rl):
     assert not missing, missing
     # and the Python binding covers the whole header
     assert set(names) <= set(rl.SIGNATURES), set(names) - set(rl.SIGNATURES)
-    assert rl.lib().rl_abi_version() == 1
+    assert rl.lib().rl_abi_version() == 2
 
 
 ENV_CASES = [("frozen_lake_4x4_det", dict(env="frozen_lake", map8x8=0, slippery=0)),
@@ -44,7 +44,11 @@ ENV_CASES = [("frozen_lake_4x4_det", dict(env="frozen_lake", map8x8=0, slippery=
              ("frozen_lake_8x8_det", dict(env="frozen_lake", map8x8=1, slippery=0)),
              ("frozen_lake_8x8_slippery", dict(env="frozen_lake", map8x8=1, slippery=1)),
              ("cliff_walking", dict(env="cliff_walking")),
-             ("taxi", dict(env="taxi"))]
+             ("taxi", dict(env="taxi")),
+             ("frozen_lake_edited_4x4_det", dict(env="frozen_lake_edited", map8x8=0, slippery=0)),
+             ("frozen_lake_edited_4x4_slippery", dict(env="frozen_lake_edited", map8x8=0, slippery=1)),
+             ("frozen_lake_edited_8x8_det", dict(env="frozen_lake_edited", map8x8=1, slippery=0)),
+             ("frozen_lake_edited_8x8_slippery", dict(env="frozen_lake_edited", map8x8=1, slippery=1))]
 
 
 @pytest.mark.parametrize("name,kw", ENV_CASES, ids=[c[0] for c in ENV_CASES])
@@ -95,3 +99,36 @@ def test_no_cpu_fallback_without_gpu(rl):
     with pytest.raises(rl.RLError) as e:
         rl.Agent(rl.default_params())
     assert e.value.code == 3          # RL_E_HIP
+
+
+@pytest.mark.parametrize("map8", [0, 1])
+def test_fl_obs_features_match_fixture(rl, oracle, map8):
+    """FrozenLakeObs input adapter (frozen_lake_neural.rs:136-145): host table ==
+    independent restatement == oracle"""
+    name = f"frozen_lake_edited_{'8x8' if map8 else '4x4'}_det"
+    g = np.array(GOLD[name]["fl_obs"])
+    for env in ("frozen_lake_edited", "frozen_lake"):
+        p = dict(env=env, map8x8=map8, net_input="fl_obs", policy="neural")
+        assert np.array_equal(rl.net_features(rl.default_params(**p)), g)
+        assert np.array_equal(oracle.net_features(oracle.default_params(**p)), g)
+
+
+def test_scalar_features_are_reference_obs_ids(rl):
+    f = rl.net_features(rl.default_params(env="blackjack", net_input="scalar"))
+    ids = [rl.lib().rl_obs_to_reference(3, s) for s in range(f.shape[0])]
+    assert np.array_equal(f[:, 0], np.array(ids, dtype=np.uint64).astype(np.float64))
+    f = rl.net_features(rl.default_params(env="taxi", net_input="scalar"))
+    assert np.array_equal(f[:, 0], np.arange(500, dtype=np.float64))
+    with pytest.raises(rl.RLError):   # FrozenLakeObs is a struct: no [[obs as f64]]
+        rl.net_features(rl.default_params(env="frozen_lake_edited", net_input="scalar"))
+    with pytest.raises(rl.RLError):
+        rl.net_features(rl.default_params(env="taxi", net_input="fl_obs"))
+
+
+def test_neural_config_validation(rl):
+    """bad network configs fail with RL_E_ARG before any GPU work"""
+    for kw in (dict(group_size=2), dict(net_hidden=0), dict(net_hidden=4096), dict(net_act1="softmax")):
+        p = rl.default_params(policy="neural", n_lanes=4, **kw)
+        with pytest.raises(rl.RLError) as e:
+            rl.Agent(p)
+        assert e.value.code == 2, (kw, e.value)

@@ -83,7 +83,8 @@ def test_kat_ucb_bit_exact(rl, oracle):
 
 @pytest.mark.parametrize("env,map8,slip", [("frozen_lake", 0, 0), ("frozen_lake", 1, 1),
                                             ("cliff_walking", 0, 0), ("taxi", 0, 0),
-                                            ("blackjack", 0, 0)])
+                                            ("blackjack", 0, 0), ("frozen_lake_edited", 0, 0),
+                                            ("frozen_lake_edited", 1, 1)])
 def test_env_trait_streams(rl, oracle, env, map8, slip):
     """Batched Env::reset/step on the GPU == the oracle's env walked with the
     same per-lane stream and actions (obs as the reference's usize ids)."""
@@ -146,6 +147,7 @@ PRIVATE_CASES = [
     dict(env="blackjack", policy="double", algo="qlearning"),
     dict(env="blackjack", agent="traces", selector="ucb", algo="sarsa"),
     dict(env="cliff_walking", policy="double", selector="ucb", algo="expected_sarsa", agent="traces"),
+    dict(env="frozen_lake_edited", map8x8=1, slippery=1, algo="qlearning"),
 ]
 
 
@@ -190,6 +192,7 @@ SHARED_CASES = [
     dict(env="blackjack", policy="double", algo="qlearning", group_size=256),
     dict(env="cliff_walking", policy="double", selector="ucb", algo="sarsa", group_size=64),
     dict(env="frozen_lake", agent="traces", policy="double", algo="qlearning", group_size=2),
+    dict(env="frozen_lake_edited", map8x8=1, algo="expected_sarsa", group_size=128),
 ]
 
 
@@ -339,4 +342,89 @@ def test_throughput_variant_matches_oracle(rl, oracle, case):
         dn, dt = dev.ucb()
         rn, rt = ref.ucb()
         assert np.array_equal(dn, rn) and dt == rt
+    _assert_stats_equal(dev, ref)
+
+
+# ---------------------------------------------------------------- NeuralPolicy
+ACTS = ["linear", "tanh", "relu", "leaky_relu", "relu6", "leaky_relu6", "sigmoid", "swish", "hard_swish"]
+
+
+def test_kat_activations_bit_exact(rl, oracle):
+    """device f, f' (src/network/activation.rs, fdlibm exp/tanh) == the oracle's"""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.normal(0, 4, 20000), rng.uniform(-800, 800, 2000), np.linspace(-7, 7, 1401),
+                        [0.0, -0.0, 6.0, -3.0, np.inf, -np.inf, np.nan, 1e-310]])
+    for a in ACTS:
+        df, dfp = rl.kat_act(a, x)
+        rf, rfp = oracle.act(a, x)
+        for d, r in ((df, rf), (dfp, rfp)):
+            same = (d.view(np.uint64) == r.view(np.uint64)) | (np.isnan(d) & np.isnan(r))
+            assert same.all(), (a, x[~same][:5], d[~same][:5], r[~same][:5])
+
+
+NEURAL_CASES = [
+    # the neural bin (src/bin/frozen_lake_neural.rs): FL 4x4, 1-32-4 leaky_relu6/linear,
+    # Q-learning, eps-greedy with the `a * 0.5` decay
+    dict(env="frozen_lake", algo="qlearning", decay_kind=1, eps_decay=0.5),
+    dict(env="frozen_lake_edited", map8x8=1, slippery=1, net_input="fl_obs", algo="sarsa", net_act1="tanh"),
+    dict(env="cliff_walking", agent="traces", algo="qlearning", net_act1="relu", net_hidden=16),
+    dict(env="taxi", selector="ucb", algo="expected_sarsa", net_act1="sigmoid", net_hidden=8),
+    dict(env="blackjack", algo="expected_sarsa", net_act1="swish", net_act2="softmax", net_hidden=12),
+    dict(env="frozen_lake", map8x8=1, algo="qlearning", net_act1="hard_swish", net_act2="leaky_relu"),
+]
+
+
+@pytest.mark.parametrize("case", NEURAL_CASES, ids=lambda c: "-".join(f"{v}" for v in c.values()))
+def test_neural_policy_matches_oracle(rl, oracle, case):
+    """NeuralPolicy agents (private): step streams, TD errors, every lane's
+    parameters and get_values of every state bit-exact vs the oracle; lane 3
+    is the faithful single-agent loop; Agent::reset re-draws the network."""
+    n_ep = 30 if case["env"] != "blackjack" else 120
+    kw = dict(net_hidden=32, max_steps=40)
+    kw.update(case)
+    p = _params(rl, policy="neural", n_lanes=45, group_size=1, sync_every=40, n_episodes_for_decay=n_ep, **kw)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    assert np.array_equal(dev.weights().view(np.uint64), ref.weights().view(np.uint64)), "init"
+    dev.set_recording(True)
+    ref.set_record(True)
+    dev.train(n_ep, n_ep // 3)
+    ref.train_episodes(n_ep, n_ep // 3)
+    _assert_records_equal(dev.records(), ref.records())
+    dw, rw = dev.weights(), ref.weights()
+    same = (dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))
+    assert same.all()
+    _assert_q_equal(dev.q(), ref.q())
+    assert np.array_equal(dev.epsilon().view(np.uint64), ref.lane_eps().view(np.uint64))
+    _assert_stats_equal(dev, ref)
+    f = oracle.Faithful(dict(p, lane_offset=3))
+    f.train(n_ep, n_ep // 3)
+    fw = f.weights()
+    assert ((fw.view(np.uint64) == dw[3].view(np.uint64)) | (np.isnan(fw) & np.isnan(dw[3]))).all()
+    dev.reset()
+    ref.reset()
+    assert np.array_equal(dev.weights().view(np.uint64), ref.weights().view(np.uint64)), "reset"
+    dev.train(n_ep // 3, 0)
+    ref.train_episodes(n_ep // 3, 0)
+    dw, rw = dev.weights(), ref.weights()
+    assert ((dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))).all()
+
+
+def test_neural_weights_roundtrip_and_dyna(rl, oracle):
+    """set_weights (Layer::set_weights) then training stays in lockstep; Dyna
+    planning over a neural policy (InternalModelAgent) matches too."""
+    p = _params(rl, policy="neural", env="cliff_walking", n_lanes=20, group_size=1, sync_every=30,
+                n_episodes_for_decay=20, net_hidden=16, max_steps=50, lr=0.001)   # finite weights
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    w = np.random.default_rng(9).normal(0, 0.05, dev.weights().shape)
+    dev.set_weights(w)
+    ref.set_weights(w)
+    assert np.array_equal(dev.weights(), w)
+    dev.set_planning(3)
+    ref.set_planning(3)
+    dev.train(15, 5)
+    ref.train_episodes(15, 5)
+    dw, rw = dev.weights(), ref.weights()   # NaN payloads differ between gfx950 and x86: NaN-aware
+    assert ((dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))).all()
     _assert_stats_equal(dev, ref)

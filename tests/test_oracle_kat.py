@@ -21,7 +21,11 @@ ENV_CASES = [("frozen_lake_4x4_det", dict(env="frozen_lake", map8x8=0, slippery=
              ("frozen_lake_8x8_det", dict(env="frozen_lake", map8x8=1, slippery=0)),
              ("frozen_lake_8x8_slippery", dict(env="frozen_lake", map8x8=1, slippery=1)),
              ("cliff_walking", dict(env="cliff_walking")),
-             ("taxi", dict(env="taxi"))]
+             ("taxi", dict(env="taxi")),
+             ("frozen_lake_edited_4x4_det", dict(env="frozen_lake_edited", map8x8=0, slippery=0)),
+             ("frozen_lake_edited_4x4_slippery", dict(env="frozen_lake_edited", map8x8=0, slippery=1)),
+             ("frozen_lake_edited_8x8_det", dict(env="frozen_lake_edited", map8x8=1, slippery=0)),
+             ("frozen_lake_edited_8x8_slippery", dict(env="frozen_lake_edited", map8x8=1, slippery=1))]
 
 
 @pytest.mark.parametrize("name,kw", ENV_CASES, ids=[c[0] for c in ENV_CASES])
