@@ -189,22 +189,32 @@ struct AgentSpec {
     std::vector<RunSpec> runs;
 };
 
+// what differs between the bins' agents: the policy (TabularPolicy(lr, 0.0) or
+// the neural bin's NeuralPolicy), the ε-decay closure and the final evaluate()
+struct PolicySpec {
+    int policy = RL_POLICY_TABULAR;
+    rl_network_config net{};
+    bool mul_decay = false;      // `a * exploration_time` (frozen_lake_neural.rs:181), else `a - ε0/(t·n)`
+    uint64_t eval_episodes = 0;  // final evaluate(): 0 = n_episodes (frozen_lake.rs:201), 1000 in the neural bin
+};
+
 // src/bin/frozen_lake.rs:139-216: TabularPolicy(lr, 0.0); ε-greedy with decay
 // `a - ε0/(exploration_time·n)` or UCB(c); each run trains n episodes (eval
 // every n/10), prints `{legend} {elapsed:.2?}`, then evaluates n episodes.
 inline int run_agents(const Flags &f, const rl_env_config &env, const std::vector<AgentSpec> &specs,
-                      const AfterTrain &after = nullptr) {
+                      const AfterTrain &after = nullptr, const PolicySpec &pol = PolicySpec()) {
     const uint64_t n = f.u64("n_episodes");
     const size_t maw = (size_t)f.u64("moving_average_window");
     rl_agent_config c{};
     c.env = env;
-    c.policy = RL_POLICY_TABULAR;
-    c.decay_kind = RL_DECAY_LINEAR;
+    c.policy = pol.policy;
+    c.net = pol.net;
+    c.decay_kind = pol.mul_decay ? RL_DECAY_MUL : RL_DECAY_LINEAR;
     c.lr = f.f64("learning_rate");
     c.gamma = f.f64("discount_factor");
     c.lambda = f.f64("lambda_factor");
     c.eps0 = f.f64("initial_epsilon");
-    c.eps_decay = c.eps0 / (f.f64("exploration_time") * (double)n);
+    c.eps_decay = pol.mul_decay ? f.f64("exploration_time") : c.eps0 / (f.f64("exploration_time") * (double)n);
     c.eps_final = f.f64("final_epsilon");
     c.ucb_c = f.f64("confidence_level");
     c.q_default = 0.0;
@@ -245,7 +255,7 @@ inline int run_agents(const Flags &f, const rl_env_config &env, const std::vecto
                             rust_f64(ex.length[0]).c_str());
             }
             if (after) after(agent, run.legend);
-            rlamd::Histories e = agent.evaluate(n);
+            rlamd::Histories e = agent.evaluate(pol.eval_episodes ? pol.eval_episodes : n);
             te_r.push_back(moving_average(maw ? n / maw : 0, e.reward));
             te_l.push_back(moving_average(maw ? n / maw : 0, e.length));
             agent.reset();

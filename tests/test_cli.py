@@ -23,7 +23,8 @@ COMMON = ["show_example", "n_episodes", "learning_rate", "initial_epsilon", "exp
           "final_epsilon", "confidence_level", "discount_factor", "lambda_factor", "moving_average_window"]
 FLAGS = {"frozen_lake": COMMON + ["stochastic_env", "map", "max_steps"],
          "taxi": COMMON + ["max_steps"], "cliffwalking": COMMON + ["max_steps"],
-         "cliffwalking_model": COMMON + ["max_steps"], "blackjack": COMMON}
+         "cliffwalking_model": COMMON + ["max_steps"], "blackjack": COMMON,
+         "frozen_lake_neural": COMMON + ["max_steps"]}
 
 SWEEP = [("one_step", 0, [(s, a) for s in ("eps_greedy", "ucb") for a in ("sarsa", "qlearning", "expected_sarsa")]),
          ("traces", 0, [(s, a) for s in ("eps_greedy", "ucb") for a in ("sarsa", "qlearning", "expected_sarsa")])]
@@ -77,7 +78,7 @@ def test_cli_fails_loudly_without_gpu(built, rl):
     assert r.returncode != 0 and "rl_agent_create" in r.stderr
 
 
-def _oracle_sweep(oracle, env_kw, n, maw, specs=SWEEP, lanes=1):
+def _oracle_sweep(oracle, env_kw, n, maw, specs=SWEEP, lanes=1, eval_n=None):
     """The bins' sequence on the oracle (lane 0 histories from step records)."""
     import oracle_ffi as O
     want = {k: [] for k in ("Train Rewards", "Train Episodes Length", "Training Error", "Test Rewards",
@@ -112,7 +113,7 @@ def _oracle_sweep(oracle, env_kw, n, maw, specs=SWEEP, lanes=1):
             want["Train Rewards"].append(ref_moving_average(n // maw, rew))
             want["Train Episodes Length"].append(ref_moving_average(n // maw, ln))
             b.set_record(True)
-            b.evaluate(n)
+            b.evaluate(eval_n or n)
             recs = b.records()[:, 0]
             b.set_record(False)
             rew, ln = [], []
@@ -138,20 +139,26 @@ def _read_csv(path):
     return rows[0], [[float(x) for x in c if x != ""] for c in cols]
 
 
+NEURAL_BIN = dict(env="frozen_lake", map8x8=0, policy="neural", decay_kind=1, eps_decay=0.5)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("prog,env_kw,specs", [("frozen_lake", dict(env="frozen_lake", map8x8=0), SWEEP),
                                                ("cliffwalking", dict(env="cliff_walking"), SWEEP),
-                                               ("cliffwalking_model", dict(env="cliff_walking"), MODEL)],
-                         ids=["frozen_lake", "cliffwalking", "cliffwalking_model"])
+                                               ("cliffwalking_model", dict(env="cliff_walking"), MODEL),
+                                               ("frozen_lake_neural", NEURAL_BIN, [MODEL[0]])],
+                         ids=["frozen_lake", "cliffwalking", "cliffwalking_model", "frozen_lake_neural"])
 def test_cli_sweep_matches_oracle(built, oracle, tmp_path, prog, env_kw, specs):
+    """frozen_lake_neural: NeuralPolicy 1-32-4, `a * 0.5` decay, evaluate(1000) (frozen_lake_neural.rs)"""
     n, maw = 40, 10
+    eval_n = 1000 if prog == "frozen_lake_neural" else None
     out = subprocess.run([os.path.join(built, prog), "-n", str(n), "--moving_average_window", str(maw),
                           "--out_dir", str(tmp_path)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr
     lines = out.stdout.strip().split("\n")
     n_runs = sum(len(r) for _, _, r in specs)
     assert len(lines) == n_runs and lines[0].startswith("ε-Greedy One-Step ")
-    want = _oracle_sweep(oracle, env_kw, n, maw, specs)
+    want = _oracle_sweep(oracle, env_kw, n, maw, specs, eval_n=eval_n)
     for title, series in want.items():
         header, got = _read_csv(os.path.join(tmp_path, title + ".csv"))
         assert len(header) == n_runs
