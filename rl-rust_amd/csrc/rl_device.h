@@ -446,7 +446,15 @@ struct EnvTables {
     double th1, th2, th3, trunc_reward;   // trunc_reward: host-side record only (the envs' own constants)
     int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
     int32_t slippery;      // FrozenLake: the map has stochastic rows (uniform per launch)
+    uint32_t S;            // |S|: row stride of an action-major table (AM layout below)
 };
+// Transition-table index of (s, a): state-major trans[s*A + a] (HBM, the private
+// kernel), or action-major trans[a*S + s] (AM: the shared kernel's LDS copy, where
+// lanes of one wave in neighbouring states then hit distinct LDS banks).
+template <bool AM, int A>
+__device__ __forceinline__ uint32_t tidx(const EnvTables &t, uint32_t s, uint32_t a) {
+    return AM ? a * t.S + s : s * (uint32_t)A + a;
+}
 // Env::reset's categorical draw (frozen_lake.rs:107-108, taxi.rs:136-137): the
 // uniform is always consumed; the search is skipped when the answer is fixed.
 __device__ __forceinline__ uint32_t start_state(const EnvTables &t, double u) {
@@ -457,21 +465,59 @@ template <int ENV> struct EnvDev;
 
 // FrozenLakeEnv (src/env/frozen_lake.rs).  trans[s*4+a]: 3 outcome bytes
 // (bits 0-5 next, bit 6 reward==1.0, bit 7 terminated) + bit 24 "slippery row".
+// One synchronous step of a FrozenLake-family lane that either RESETs (doR) or
+// STEPs (doS), without branching on which: both consume exactly one uniform
+// (reset :107-108 / :222-223, step :126 / :235) unless the step truncates, so
+// the draw is one masked block for the wave, and the table word is read by
+// every lane (pos and a are always valid indices).  Truncation: (0, 0.0, true)
+// for FrozenLake (:119-122), (pos, -1.0, true) for FrozenLakeEdited (:227-231).
+// The outcome byte's reward bit means 1.0 (FrozenLake) or 10.0 (edited; else -1.0).
+template <bool EDITED, int SLIP, bool AM>
+__device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
+                                           const EnvTables &t, uint32_t &s2, double &rew, bool &term) {
+    const bool trunc = doS && z >= t.max_steps;
+    const bool st = doS && !trunc;
+    const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
+    uint32_t i = 0;
+    if (doR || st) {
+        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {
+            const double u = uniform01(r);
+            if (st && (w & (1u << 24))) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
+        } else {
+            r.skip_u32();
+            r.skip_u32();
+        }
+    }
+    const uint32_t o = (w >> (8 * i)) & 0xffu;
+    const double r_bit = EDITED ? 10.0 : 1.0, r_else = EDITED ? -1.0 : 0.0;
+    s2 = st ? (o & 63u) : ((EDITED && trunc) ? pos : 0u);
+    rew = st ? ((o & 64u) ? r_bit : r_else) : ((EDITED && trunc) ? -1.0 : 0.0);
+    term = trunc || (st && (o & 128u) != 0u);
+    z = doR ? 0u : (st ? z + 1u : z);
+    pos = s2;
+}
+
+// Both built-in maps (MAP_4X4 / MAP_8X8) have one 'S', at position 0, so
+// Env::reset's categorical draw always returns 0 (the host asserts this): the
+// draw is consumed without computing its value.  SLIP: the map's slippery
+// flag as a compile-time constant (0 / 1), or -1 to read it at run time.
 template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
     static constexpr int A = 4;
-    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
-        const double u = uniform01(r);                 // frozen_lake.rs:107-108
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &) {
+        r.skip_u32();                                  // frozen_lake.rs:107-108: one uniform,
+        r.skip_u32();                                  // categorical_sample -> 0
         z = 0;
-        return start_state(t, u);
+        return 0u;
     }
+    template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :119-122
         z += 1;
-        const uint32_t w = t.trans[pos * 4 + a];
+        const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
         uint32_t i = 0;
-        if (t.slippery) {                              // :126, drawn even when not slippery
+        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {   // :126, drawn even when not slippery
             const double u = uniform01(r);
             if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
         } else {
@@ -492,19 +538,21 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
 // observes the current position with -1.0 (:227-231); one draw per step (:235).
 template <> struct EnvDev<RL_ENV_FROZEN_LAKE_EDITED> {
     static constexpr int A = 4;
-    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
-        const double u = uniform01(r);                 // :222-223
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &) {
+        r.skip_u32();                                  // :222-223, the start is position 0
+        r.skip_u32();                                  // (same maps as FrozenLakeEnv)
         z = 0;
-        return start_state(t, u);
+        return 0u;
     }
+    template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = pos; rew = -1.0; term = true; return; }
         z += 1;
-        const uint32_t w = t.trans[pos * 4 + a];
+        const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
         uint32_t i = 0;
-        if (t.slippery) {
+        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {
             const double u = uniform01(r);
             if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
         } else {
@@ -527,12 +575,13 @@ template <> struct EnvDev<RL_ENV_CLIFF_WALKING> {
         z = 0;
         return 36u;                                    // cliff_walking.rs:71
     }
+    template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = 0; rew = -100.0; term = true; return; }  // :81-84
         z += 1;
-        const uint32_t w = t.trans[pos * 4 + a];
+        const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
         s2 = w & 63u;
         rew = (w & 64u) ? -100.0 : -1.0;
         term = (w & 128u) != 0;
@@ -549,12 +598,13 @@ template <> struct EnvDev<RL_ENV_TAXI> {
         z = 0;
         return start_state(t, u);
     }
+    template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
                                                 const EnvTables &t, uint32_t &s2, double &rew,
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :146-149
         z += 1;
-        const uint32_t w = t.trans[pos * 6 + a];
+        const uint32_t w = t.trans[tidx<AM, 6>(t, pos, a)];
         s2 = w & 511u;
         const uint32_t rc = (w >> 9) & 3u;
         rew = rc == 0 ? -1.0 : (rc == 1 ? -10.0 : 20.0);
@@ -585,6 +635,7 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         const uint32_t pa = (z >> 20) & 1u;
         return obs(score(z & 0xffu, pa), (z >> 16) & 0xfu, pa);
     }
+    template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
                                                 const EnvTables &, uint32_t &s2, double &rew,
                                                 bool &term) {

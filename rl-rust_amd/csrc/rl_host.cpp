@@ -212,6 +212,8 @@ int build_env(const rl_env_config &c, EnvHost &e) {
         return fail(RL_E_ARG, "unknown env kind");
     }
     if (!e.start.empty()) finish_cdf(e);
+    // the device FrozenLake resets assume the built-in maps' single start at 0 (rl_device.h)
+    if (e.map && e.fixed_start != 0) return fail(RL_E_ARG, "FrozenLake map must start at position 0");
     return RL_OK;
 }
 

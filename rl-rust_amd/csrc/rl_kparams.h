@@ -6,6 +6,10 @@
 
 #include "rl.h"
 
+#ifndef RLAMD_EXP
+#define RLAMD_EXP 0
+#endif
+
 namespace rlamd {
 
 // Q fixed point for the shared (group_size > 1) mode: value = raw * 2^-QFRAC.

@@ -268,7 +268,7 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // ======================================================================== shared
 // INSTR: step records / episode log compiled in (chosen at launch when either is
 // enabled); the throughput variant carries neither.
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -296,18 +296,31 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     double *RCP = (double *)(smem + lay.rcp);
 
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
+    // LDS table layout: state-major [tbl][s][a] like HBM (LDS_AM = false), or
+    // action-major [tbl][a][s] (LDS_AM = true: measured 6 % slower on cfg 2 —
+    // 4 ds_read_b64 per row instead of 2 ds_read_b128 cost more than the bank
+    // conflicts they avoid).
+    constexpr bool LDS_AM = false;
+    auto qi = [&](uint32_t tbl, uint32_t s, uint32_t a) -> uint32_t {
+        return LDS_AM ? tbl * SA + a * S + s : tbl * SA + s * (uint32_t)A + a;
+    };
+    auto lds_of = [&](uint32_t i) -> uint32_t {        // HBM index -> LDS index
+        if constexpr (!LDS_AM) return i;
+        const uint32_t tbl = i / SA, r = i - tbl * SA;
+        return qi(tbl, r / (uint32_t)A, r % (uint32_t)A);
+    };
     if (tid < 8) ACC[tid] = 0ull;
     for (uint32_t i = tid; i <= nthr; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
-    for (uint32_t i = tid; i < PSA; i += nthr) { Q[i] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
+    for (uint32_t i = tid; i < PSA; i += nthr) { Q[lds_of(i)] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
     for (uint32_t i = tid; i < (PSA + 1u) / 2u; i += nthr) CNT[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
-        for (uint32_t i = tid; i < PSA; i += nthr) QF8[i] = (uint8_t)p.qf_base[i];
-        for (uint32_t i = tid; i < SA; i += nthr) N[i] = p.n_base[i];
+        for (uint32_t i = tid; i < PSA; i += nthr) QF8[lds_of(i)] = (uint8_t)p.qf_base[i];
+        for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = p.n_base[i];
         if (tid == 0) T[0] = p.t_base[0];
     }
     if constexpr (ENV != RL_ENV_BLACKJACK)
-        for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
+        for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
     if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
         for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
@@ -317,6 +330,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
     tabs.slippery = p.slippery;
+    tabs.S = S;
 
     const uint64_t lane = (uint64_t)blockIdx.x * p.G + tid;
     const bool active = tid < p.G && lane < p.L;
@@ -334,8 +348,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     auto load_rows = [&](uint32_t s, int64_t (&ra)[A], int64_t (&rb)[A]) {
 #pragma unroll
         for (int i = 0; i < A; ++i) {
-            ra[i] = (int64_t)Q[s * A + i];
-            rb[i] = P == 2 ? (int64_t)Q[SA + s * A + i] : 0;
+            ra[i] = (int64_t)Q[qi(0, s, i)];
+            rb[i] = P == 2 ? (int64_t)Q[qi(1, s, i)] : 0;
         }
     };
     // Agent::get_action = selector(Policy::predict(s)) against the step snapshot;
@@ -352,9 +366,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             const double lnt = rl_log((double)T[0]);
 #pragma unroll
             for (int i = 0; i < A; ++i) {
-                double v = val(s * A + i, ra[i]);
-                if constexpr (P == 2) v = (v + val(SA + s * A + i, rb[i])) / 2.0;
-                u[i] = ucb_value(v, p.ucb_c, lnt, (double)N[s * A + i]);
+                double v = val(qi(0, s, i), ra[i]);
+                if constexpr (P == 2) v = (v + val(qi(1, s, i), rb[i])) / 2.0;
+                u[i] = ucb_value(v, p.ucb_c, lnt, (double)N[qi(0, s, i)]);
             }
             return argmax<A>(u);
         }
@@ -397,19 +411,28 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         double r = 0.0;
         bool term = false;
         int64_t ra2[A], rb2[A];
-        if (doR) {
+        if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED) {
+            uint32_t pos = L.s;                    // reset or step in one predicated block
+            fl_advance<ENV == RL_ENV_FROZEN_LAKE_EDITED, SLIP, LDS_AM>(doR, doS, pos, L.z, L.a, L.rng, tabs, s2, r,
+                                                                       term);
+            L.ready = doR ? true : (term ? false : L.ready);
+        } else if (doR) {
             s2 = E::reset(L.z, L.rng, tabs);
             L.ready = true;
         } else if (doS) {
             uint32_t pos = L.s;
-            E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
+            E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
         load_rows(s2, ra2, rb2);                   // s2 == 0 (a valid row) on idle lanes
+#if RLAMD_EXP & 4   // timing experiment: greedy selection, no RNG (results differ)
+        if (alive) { int64_t v[A]; for (int i = 0; i < A; ++i) v[i] = ra2[i]; a2 = argmax_i64<A>(v); }
+#else
         if (alive) a2 = select(s2, ra2, rb2);
+#endif
         if constexpr (UCB) {
             __syncthreads();
-            if (alive) atomicAdd(&N[s2 * A + a2], 1u);
+            if (alive) atomicAdd(&N[qi(0, s2, a2)], 1u);
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
             __syncthreads();
@@ -432,7 +455,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             } else {
                 double q2[A], pr[A];
 #pragma unroll
-                for (int i = 0; i < A; ++i) q2[i] = val(vt * SA + s2 * A + i, rv[i]);
+                for (int i = 0; i < A; ++i) q2[i] = val(qi(vt, s2, i), rv[i]);
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
@@ -440,7 +463,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     double sum = 0.0;
 #pragma unroll
                     for (int i = 0; i < A; ++i) {
-                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)N[s2 * A + i]);
+                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)N[qi(0, s2, i)]);
                         sum += pr[i];
                     }
 #pragma unroll
@@ -448,22 +471,30 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
                 fq = future_q<ALGO, A>(q2, a2, pr);
             }
-            const uint32_t qidx = vt * SA + L.s * A + L.a;
+            const uint32_t qidx = qi(vt, L.s, L.a);
             const double qa = val(qidx, (int64_t)Q[qidx]);
             td = r + p.gamma * fq - qa;
         }
         if constexpr (!TRACES) {
-            const uint32_t idx = ut * SA + L.s * A + L.a;
+            const uint32_t idx = qi(ut, L.s, L.a);
             bool owner = false;
             if (train) {
                 uint32_t fl = 0;
                 int64_t dq;
                 if constexpr (SPEC) dq = q_fix(p.lr * td, fl);
                 else dq = q_fix_finite(p.lr * td);
+#if RLAMD_EXP & 2   // timing experiment: no LDS atomics (results differ)
+                owner = dq == 12345;
+#else
                 owner = contribute(idx, dq, 1u, fl);
+#endif
             }
             __syncthreads();   // all contributions in, all Q reads done
+#if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
+            if (sweep) { if (tid < PSA && CNT16[tid] == 77) settle(tid); }
+#else
             if (sweep) { if (tid < PSA) settle(tid); }
+#endif
             else if (owner) settle(idx);
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
@@ -478,7 +509,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 int64_t d;
                 if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
                 else d = q_fix_finite(p.lr * (td * ev));
-                const uint32_t idx = ut * SA + o * A + b;
+                const uint32_t idx = qi(ut, o, b);
                 if (contribute(idx, d, 1u, fl) && !sweep) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
             });
             if (train && term) tcnt = 0;                  // the trace map is cleared
@@ -543,7 +574,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     int64_t *const dl = p.delta_rep + (uint64_t)(blockIdx.x % p.n_rep) * p.delta_words;
     __syncthreads();
     for (uint32_t i = tid; i < PSA; i += nthr) {
-        const int64_t d = (int64_t)(Q[i] - (unsigned long long)p.q_base[i]);
+        const int64_t d = (int64_t)(Q[lds_of(i)] - (unsigned long long)p.q_base[i]);
         if (d) {
             atomicAdd((unsigned long long *)&dl[i], (unsigned long long)d);
             atomicAdd((unsigned long long *)&dl[PSA + i], 1ull);
@@ -551,7 +582,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < SA; i += nthr) {
-            const int64_t d = (int64_t)N[i] - (int64_t)p.n_base[i];
+            const int64_t d = (int64_t)N[lds_of(i)] - (int64_t)p.n_base[i];
             if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + i], (unsigned long long)d);
         }
         if (tid == 0) {
@@ -561,7 +592,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (SPEC) {
             int64_t *fc = dl + 2 * PSA + SA + 1;
             for (uint32_t i = tid; i < PSA; i += nthr) {
-                const uint32_t nf = QF8[i] & ~p.qf_base[i];
+                const uint32_t nf = QF8[lds_of(i)] & ~p.qf_base[i];
                 if (nf & QF_NAN) atomicAdd((unsigned long long *)&fc[i], 1ull);
                 if (nf & QF_PINF) atomicAdd((unsigned long long *)&fc[PSA + i], 1ull);
                 if (nf & QF_NINF) atomicAdd((unsigned long long *)&fc[2 * PSA + i], 1ull);
@@ -577,9 +608,9 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
 // FrozenLake / CliffWalking.  The other variants would spill for no occupancy.
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP>(p);
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
@@ -825,8 +856,17 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
     } else if (instr) {
         k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, true>;
     } else {
-        if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO>;
-        else k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+        if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) {
+            // the map's slippery flag as a compile-time constant (FrozenLake only)
+            if constexpr (ENV == RL_ENV_FROZEN_LAKE) {
+                if (!p.slippery) k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0>;
+                else k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1>;
+            } else {
+                k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1>;
+            }
+        } else {
+            k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+        }
     }
     if (smem > 64 * 1024) {   // gfx950: a workgroup may use up to the CU's 160 KiB of LDS
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# build librlamd with the FrozenLake TU compiled under -DRLAMD_EXP=<mask> (timing
+# experiments only: the masked variants compute WRONG results) into rl-rust_amd/exp/
+set -e
+cd "$(dirname "$0")/../rl-rust_amd"
+mkdir -p exp
+for m in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../include -fPIC -ffp-contract=off -fno-fast-math -Wall \
+     -Wno-unused-result -mllvm -amdgpu-atomic-optimizer-strategy=None -DRLAMD_EXP=$m -c csrc/rl_train_frozen_lake.hip -o exp/fl_$m.o &
+done
+wait
+for m in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o exp/librlamd_$m.so exp/fl_$m.o \
+     build/rl_train_cliff_walking.hip.o build/rl_train_taxi.hip.o build/rl_train_blackjack.hip.o \
+     build/rl_train_frozen_lake_edited.hip.o build/rl_misc.hip.o build/rl_host.cpp.o
+done
+rm -f exp/*.o
+ls -la exp
