@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1] = SURVEY §8(d) cfg 2): FrozenLake-8x8
 (deterministic), one-step Q-learning, eps-greedy, 2^20 lanes per GPU, learner
-groups of 256 lanes (one workgroup, Q in LDS), merge every K=64 synchronous
+groups of 512 lanes (one workgroup, Q in LDS), merge every K=64 synchronous
 steps.  One bench "step" = one launch = K synchronous env-steps of every lane +
 the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
 §8(d): warm-up 64 synchronous steps (1 launch), timed window 4,096 (64 launches).
@@ -59,7 +59,7 @@ def parse():
 # SURVEY §8(d) workloads; lanes are per GPU (cfg 4: 2^19 over 4 GPUs, cfg 5: 2^22 over 8)
 PRESETS = {
     2: dict(env="frozen_lake", agent="one_step", policy="tabular", selector="eps_greedy",
-            algo="qlearning", lanes=1 << 20, group=256),
+            algo="qlearning", lanes=1 << 20, group=512),
     3: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="expected_sarsa",
             lanes=1 << 20, group=1024),
     4: dict(env="cliff_walking", agent="traces", policy="tabular", selector="eps_greedy", algo="sarsa",

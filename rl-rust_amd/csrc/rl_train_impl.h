@@ -268,7 +268,7 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // ======================================================================== shared
 // INSTR: step records / episode log compiled in (chosen at launch when either is
 // enabled); the throughput variant carries neither.
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -377,7 +377,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // fits the block, PSA <= nthr): thread i settles entry i every step, so the
     // counter add needs no return value.  Owner form: the step's first
     // contributor (old count 0) settles the entry.
-    const bool sweep = PSA <= nthr;
+    const bool sweep = SWEEP == 1 || PSA <= nthr;   // SWEEP == 1: the host checked PSA <= block
     auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
         const uint32_t sh = (idx & 1u) * 16u;
         bool first = false;
@@ -608,9 +608,9 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
 // FrozenLake / CliffWalking.  The other variants would spill for no occupancy.
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP>(p);
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
@@ -858,11 +858,17 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
     } else {
         if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) {
             // the map's slippery flag as a compile-time constant (FrozenLake only)
+            // the map's slippery flag (FrozenLake) and the settle form (every entry
+            // owned by one thread when P*S*A <= block size) as compile-time constants
+            const bool sw = p.P * p.S * p.A <= block.x;
             if constexpr (ENV == RL_ENV_FROZEN_LAKE) {
-                if (!p.slippery) k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0>;
-                else k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1>;
+                if (!p.slippery) k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0, 1>
+                                        : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0, -1>;
+                else k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1, 1>
+                            : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1, -1>;
             } else {
-                k = (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1>;
+                k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>
+                       : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>;
             }
         } else {
             k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
