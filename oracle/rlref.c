@@ -1340,12 +1340,12 @@ struct rlo_batch {
     uint32_t net_gen;
 };
 
-/* Fixed-point Q (shared mode).  |Q raw| <= 2^52, so every entry converts to
+/* Fixed-point Q (shared mode).  |Q raw| <= 2^51, so every entry converts to
  * f64 exactly and (a+b)/2 of two entries is exact too: comparisons on raw
  * int64 values are then identical to the reference's f64 comparisons.
  * delta -> raw: NaN/inf become sticky flags; finite values are clamped to
  * +-2^51 and rounded half-to-even. */
-#define Q_RAW_MAX ((int64_t)1 << 52)
+#define Q_RAW_MAX ((int64_t)1 << 51)   /* |Q| <= 2048 */
 #define D_RAW_MAX 0x1p51
 static int64_t q_fix(double d, uint8_t *flag) {
     if (d != d) { *flag |= QF_NAN; return 0; }

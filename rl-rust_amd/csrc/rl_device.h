@@ -350,10 +350,11 @@ __device__ __forceinline__ double ucb_value(double q, double c, double lnt, doub
 
 // ------------------------------------------------------------------ fixed-point Q
 // Shared-mode Q entries are int64 fixed point, value = raw * 2^-40, clamped to
-// |raw| <= 2^52 (|Q| <= 4096): every entry — and (a+b)/2 of two entries —
-// converts to f64 exactly, so comparisons on raw int64 are identical to the
-// reference's f64 comparisons (argmax / max without conversions).
-constexpr int64_t Q_RAW_MAX = (int64_t)1 << 52;
+// |raw| <= 2^51 (|Q| <= 2048; |r| <= 100 and gamma = 0.95 keep every reference
+// env's Q within 2000): every entry — and (a+b)/2 of two entries — converts to
+// f64 exactly, so comparisons on raw int64 are identical to the reference's
+// f64 comparisons (argmax / max without conversions).
+constexpr int64_t Q_RAW_MAX = (int64_t)1 << 51;
 
 // finite delta -> raw: d*2^40 clamped to +-2^51 then rounded half-to-even; the
 // 1.5*2^52 magic add performs rint and the f64->int64 conversion at once.
@@ -374,13 +375,17 @@ __device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag) {
 __device__ __forceinline__ int64_t q_clamp(int64_t v) {
     return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
 }
-__device__ __forceinline__ double q_val(int64_t raw) { return (double)raw * 0x1p-40; }
+// (double)raw * 2^-40 for |raw| <= 2^51 in two operations: raw added to the bits
+// of 1.5*2^12 (whose ulp is 2^-40) gives 6144 + raw*2^-40 exactly, then 6144 off.
+__device__ __forceinline__ double q_val(int64_t raw) {
+    return __longlong_as_double((long long)(0x40B8000000000000ull + (uint64_t)raw)) - 6144.0;
+}
 __device__ __forceinline__ double q_val(int64_t raw, uint32_t fl) {
     if (fl) {
         if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return __builtin_nan("");
         return (fl & QF_PINF) ? __builtin_inf() : -__builtin_inf();
     }
-    return (double)raw * 0x1p-40;
+    return q_val(raw);
 }
 template <int A>
 __device__ __forceinline__ uint32_t argmax_i64(const int64_t (&v)[A]) {

@@ -339,7 +339,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint32_t tcnt = 0, trace_states = 0;           // traces: size of the lane's visited set
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
 
-    // f64 image of entry idx (exact: |raw| <= 2^52)
+    // f64 image of entry idx (exact: |raw| <= 2^51)
     auto val = [&](uint32_t idx, int64_t raw) -> double {
         if constexpr (SPEC) return q_val(raw, QF8[idx]);
         else return q_val(raw);
