@@ -88,24 +88,28 @@ def cpu_baseline(args):
                              check=True, capture_output=True, text=True).stdout
         return json.loads(out)
 
-    probe = run(20000)
-    rate = probe["steps"] / max(probe["seconds"], 1e-6)
-    eps_per_sec = 20000 / max(probe["seconds"], 1e-6)
-    n = max(20000, int(eps_per_sec * args.cpu_seconds))
-    r = run(n)
+    def sized(threads, target):
+        # episode length depends on n (the eps decay spans 0.5*n episodes), so
+        # grow n until one run takes about `target` seconds
+        n, r = 20000, run(20000, threads)
+        while r["seconds"] < 0.6 * target and n < (1 << 34):
+            n = int(n * min(8.0, max(1.5, target / max(r["seconds"], 1e-3))))
+            r = run(n, threads)
+        return n, r
+
+    n, r = sized(1, args.cpu_seconds)
     res = {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": 1, "kind": "port",
            "sample": f"oracle faithful single-env loop (src/agent.rs:66-118 restated in C), "
                      f"{args.env} {'8x8' if args.map8x8 else '4x4'} {args.agent} {args.algo} "
-                     f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s "
-                     f"(probe {rate:.3g} steps/s)"}
+                     f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s"}
     # one independent faithful env per host core (the box's CPU
     # share is 16 threads; os.cpu_count() reports the whole machine)
     threads = min(16, os.cpu_count() or 1)
     if threads > 1:
-        m = run(max(20000, int(eps_per_sec * args.cpu_seconds / 4)), threads)   # episodes per thread
+        m_n, m = sized(threads, args.cpu_seconds / 2)
         res["multi_core"] = {"value": m["steps_per_sec"], "cores": threads,
-                             "sample": f"{threads} independent faithful envs, {m['steps']} env-steps "
-                                       f"in {m['seconds']:.2f} s"}
+                             "sample": f"{threads} independent faithful envs x {m_n} episodes, "
+                                       f"{m['steps']} env-steps in {m['seconds']:.2f} s"}
     return res
 
 
@@ -117,23 +121,30 @@ def main():
     import torch  # loaded before librlamd so both share one HIP runtime
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; RLAMD_DIST_BACKEND=gloo (with ranks sharing a device)
+    # rehearses the N>1 path on a one-GPU box — the driver's runs use RCCL
+    backend = os.environ.get("RLAMD_DIST_BACKEND", "nccl")
+    dev = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import rlamd
 
     p = rlamd.default_params(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
                              agent=args.agent, policy=args.policy, selector=args.selector,
                              algo=args.algo, n_lanes=args.lanes, group_size=args.group,
                              sync_every=args.sync, lane_offset=rank * args.lanes,
-                             device=local_rank)
+                             device=dev)
     agent = rlamd.Agent(p)
     stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
     torch.cuda.set_stream(stream)
     agent.set_stream(stream.cuda_stream)
     delta = None
     if world > 1:
-        delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{local_rank}")
+        delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
 
     def step():
@@ -168,11 +179,11 @@ def main():
     steps_done = st1["train_steps"] - st0["train_steps"]
     assert 0 < steps_done <= args.steps * args.sync * args.lanes, steps_done
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{dev}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     if world > 1:
-        ts = torch.tensor([steps_done], dtype=torch.int64, device=f"cuda:{local_rank}")
+        ts = torch.tensor([steps_done], dtype=torch.int64, device=f"cuda:{dev}")
         dist.all_reduce(ts)
         total_steps = int(ts.item())
     else:

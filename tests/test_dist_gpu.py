@@ -1,0 +1,71 @@
+"""N>1 rehearsal on the one-GPU box (gloo, 2 ranks sharing the device).
+
+The driver runs bench.py at N = 2/4/8 over RCCL on a whole node; these tests
+exercise the same per-rank code path on real hardware:
+  - the per-rank merge (launch_train -> all_reduce(int64 delta) -> launch_apply)
+    gives raw Q / UCB counters bit-identical to one process holding every lane;
+  - `python -m torch.distributed.run ... bench.py --gpus 2` prints one valid
+    JSON line on rank 0 (whole-job value, max-over-ranks wall time).
+Both run as child processes launched before this process touches the GPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _torchrun(args, n=2, timeout=240):
+    env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+CASES = {
+    "fl8x8-qlearning": dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256),
+    "taxi-ucb-esarsa": dict(env="taxi", selector="ucb", algo="expected_sarsa", group_size=512),
+    "cliff-traces-sarsa": dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=256),
+    "blackjack-double-q": dict(env="blackjack", policy="double", algo="qlearning", group_size=512),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_two_rank_device_merge_equals_one_process(tmp_path, name):
+    case = dict(CASES[name], sync_every=32, n_launch=4, lanes_per_rank=8192)
+    out = tmp_path / "res.json"
+    r = _torchrun([os.path.join("tests", "dist_gpu_worker.py"), str(out), json.dumps(case)])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert res["steps_ranks"] == res["steps_one"] > 0, res
+    assert res["q_nonzero"] + res["q_nonfinite"] > 0, res   # UCB+E-SARSA: all-NaN/inf is legal (F7)
+    assert res["q_equal"] and res["qf_equal"], res
+    if "ucb_equal" in res:
+        assert res["ucb_equal"], res
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_prints_one_line():
+    r = _torchrun(["bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1", "--lanes", str(1 << 16),
+                   "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["scaling"] == "weak"
+    # whole-job value: both ranks' env-steps over the max-over-ranks wall time
+    assert d["value"] > 0 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["env_steps_per_launch"] <= 64 * (1 << 16)
