@@ -61,11 +61,11 @@ PRESETS = {
     2: dict(env="frozen_lake", agent="one_step", policy="tabular", selector="eps_greedy",
             algo="qlearning", lanes=1 << 20, group=512),
     3: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="expected_sarsa",
-            lanes=1 << 20, group=1024),
+            lanes=1 << 20, group=512),
     4: dict(env="cliff_walking", agent="traces", policy="tabular", selector="eps_greedy", algo="sarsa",
             lanes=1 << 17, group=256),
     5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
-            lanes=1 << 19, group=1024),
+            lanes=1 << 19, group=512),
 }
 
 
@@ -139,6 +139,7 @@ def main():
                              sync_every=args.sync, lane_offset=rank * args.lanes,
                              device=dev)
     agent = rlamd.Agent(p)
+    occ = agent.occupancy()   # resident learner groups per CU (LDS / VGPR limited)
     stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
     torch.cuda.set_stream(stream)
     agent.set_stream(stream.cuda_stream)
@@ -216,7 +217,8 @@ def main():
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
                    "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
-                   "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}"},
+                   "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
+                   "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"]},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,

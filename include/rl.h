@@ -272,6 +272,9 @@ int rl_agent_launch_train(rl_agent *a);
 int rl_agent_launch_apply(rl_agent *a);
 /* run on a caller stream (hipStream_t as void*); NULL = the handle's own stream */
 int rl_agent_set_stream(rl_agent *a, void *stream);
+/* resident train-kernel workgroups per CU (learner groups in shared mode), the
+ * LDS bytes of one and its block size, for the kernel the next launch picks */
+int rl_agent_occupancy(rl_agent *a, uint32_t *groups_per_cu, uint64_t *lds_bytes, uint32_t *block_threads);
 /* HIP-event timing of every train kernel launch */
 int rl_agent_set_timing(rl_agent *a, int32_t enable);
 int rl_agent_get_timing(rl_agent *a, double *total_ms, uint64_t *n_launches);

@@ -452,6 +452,8 @@ struct EnvTables {
     int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
     int32_t slippery;      // FrozenLake: the map has stochastic rows (uniform per launch)
     uint32_t S;            // |S|: row stride of an action-major table (AM layout below)
+    const uint16_t *trans16 = nullptr;   // Taxi's 12-bit words as u16 in LDS (training kernels:
+                                         // half the table, two learner groups per CU)
 };
 // Transition-table index of (s, a): state-major trans[s*A + a] (HBM, the private
 // kernel), or action-major trans[a*S + s] (AM: the shared kernel's LDS copy, where
@@ -609,7 +611,7 @@ template <> struct EnvDev<RL_ENV_TAXI> {
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :146-149
         z += 1;
-        const uint32_t w = t.trans[tidx<AM, 6>(t, pos, a)];
+        const uint32_t w = t.trans16 ? (uint32_t)t.trans16[tidx<AM, 6>(t, pos, a)] : t.trans[tidx<AM, 6>(t, pos, a)];
         s2 = w & 511u;
         const uint32_t rc = (w >> 9) & 3u;
         rew = rc == 0 ? -1.0 : (rc == 1 ? -10.0 : 20.0);

@@ -461,7 +461,7 @@ int launch_train_kernel(rl_agent *a) {
         HIPC(hipEventRecord(e0, a->stream));
     }
     {
-        const hipError_t le = a->fn(a->kp, a->grid, a->block, a->smem, a->stream);
+        const hipError_t le = a->fn(a->kp, a->grid, a->block, a->smem, a->stream, nullptr);
         if (le != hipSuccess)
             return fail(RL_E_HIP, std::string("train kernel launch (smem ") + std::to_string(a->smem) +
                                       " B, block " + std::to_string(a->block.x) + "): " + hipGetErrorString(le));
@@ -1176,6 +1176,17 @@ int rl_agent_launch_apply(rl_agent *a) {
 int rl_agent_set_stream(rl_agent *a, void *stream) {
     if (!a) return fail(RL_E_ARG, "null agent");
     a->stream = stream ? (hipStream_t)stream : a->own_stream;
+    return RL_OK;
+}
+
+int rl_agent_occupancy(rl_agent *a, uint32_t *groups_per_cu, uint64_t *lds_bytes, uint32_t *block_threads) {
+    if (!a || !groups_per_cu || !lds_bytes || !block_threads) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    int n = 0;
+    HIPC(a->fn(a->kp, a->grid, a->block, a->smem, a->stream, &n));
+    *groups_per_cu = (uint32_t)n;
+    *lds_bytes = a->smem;
+    *block_threads = a->block.x;
     return RL_OK;
 }
 

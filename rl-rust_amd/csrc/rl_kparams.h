@@ -96,8 +96,10 @@ struct KParams {
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation
+// occ != nullptr: no launch; *occ = resident workgroups per CU of the kernel
+// the launch would pick (hipOccupancyMaxActiveBlocksPerMultiprocessor)
 typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, size_t smem,
-                                      hipStream_t stream);
+                                      hipStream_t stream, int *occ);
 
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start,

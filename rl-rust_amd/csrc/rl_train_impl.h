@@ -20,8 +20,31 @@ namespace rlamd {
 
 struct SmemLayout {
     uint32_t st, q, sum, cnt, qf, n, t, list, rcp, tr, cdf, total;
+    uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// Blackjack's LDS rows (shared mode, eps-greedy): the learner group's Q copy holds
+// only the states an update can write — non-terminal observations, p <= 21 and
+// dealer card d <= 10 (blackjack.rs:121-162: every other observation ends the
+// episode) — as (p*11 + d)*2 + ace, 484 of the 1728 dense rows.  Terminal rows
+// are only read (TD target / selection at s'), never written, so they are read
+// from Q_base in HBM (L2-resident).  UCB writes counters at terminal s' too, so
+// UCB keeps the dense rows.
+constexpr uint32_t BJ_LDS_STATES = 22u * 11u * 2u;
+__host__ __device__ inline bool bj_compact(int env, int ucb) { return env == RL_ENV_BLACKJACK && !ucb; }
+__host__ __device__ inline bool bj_nonterminal(uint32_t s) {
+    const uint32_t p = s / 54u, d = (s >> 1) % 27u;
+    return p <= 21u && d <= 10u;
+}
+__host__ __device__ inline uint32_t bj_row(uint32_t s) {          // dense obs -> LDS row
+    const uint32_t p = s / 54u, r = s - p * 54u;
+    return (p * 11u + (r >> 1)) * 2u + (r & 1u);
+}
+__host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> dense obs
+    const uint32_t pd = row >> 1, p = pd / 11u, d = pd - p * 11u;
+    return (p * 27u + d) * 2u + (row & 1u);
+}
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40)
 //   sum  int64 [P][S][A]   this step's summed deltas per entry
@@ -35,7 +58,11 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
                                                   uint32_t A, uint32_t n_start, uint32_t nthr) {
     const int shared_q = nthr != 0;
     SmemLayout l;
-    const uint32_t SA = S * A, PSA = (uint32_t)P * SA;
+    const uint32_t SL = (shared_q && bj_compact(env, ucb)) ? BJ_LDS_STATES : S;   // LDS rows
+    const uint32_t SA = S * A, PSA = (uint32_t)P * SL * A;
+    // full 1.0/n table when every entry is settled each step (sweep form: n can
+    // reach the group size); 64 entries for the owner form (few contributions)
+    l.nrcp = !shared_q ? 0u : (PSA <= nthr ? nthr + 1u : (nthr + 1u < 65u ? nthr + 1u : 65u));
     uint32_t off = 0;
     l.st = off; off += 64u;                       // per-block stats accumulators (u64[8])
     l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
@@ -45,8 +72,8 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.n = off; off += (shared_q && ucb) ? align16(SA * 4u) : 0u;
     l.t = off; off += (shared_q && ucb) ? 16u : 0u;
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
-    l.rcp = off; off += shared_q ? align16((nthr + 1u) * 8u) : 0u;
-    l.tr = off; off += env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
+    l.rcp = off; off += align16(l.nrcp * 8u);
+    l.tr = off; off += env == RL_ENV_TAXI ? align16(SA * 2u) : env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
     l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED || env == RL_ENV_TAXI)
                             ? align16(n_start * 8u) : 0u;
     l.total = off;
@@ -236,8 +263,8 @@ __device__ __forceinline__ void trace_visit(const KParams &p, uint64_t lane, uin
 // The eligibility sweep over slots [0, nv): E[o][b] is read, fn(o, b, E) applied,
 // E *= gamma*lambda written back.  TC slots at a time with every load issued
 // before any use (memory-level parallelism; slot j of all lanes is one row).
-template <int A, class Fn>
-__device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uint32_t nv, Fn &&fn) {
+template <int A, class RowFn, class Fn>
+__device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uint32_t nv, RowFn &&row_fn, Fn &&fn) {
     constexpr uint32_t TC = 4;
     const uint64_t Ls = p.L;
     for (uint32_t j0 = 0; j0 < nv; j0 += TC) {
@@ -255,6 +282,7 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
         for (uint32_t c = 0; c < TC; ++c) {
             if (j0 + c < nv) {
                 const uint32_t j = j0 + c;
+                row_fn(o[c]);
 #pragma unroll
                 for (int b = 0; b < A; ++b) {
                     fn(o[c], (uint32_t)b, ev[c][b]);
@@ -276,7 +304,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     constexpr bool UCB = SEL == RL_SEL_UCB;
     constexpr bool TRACES = AGENT == RL_AGENT_TRACES;
     constexpr bool SPEC = UCB && ALGO == RL_ALGO_EXPECTED_SARSA;  // inf/NaN possible
+    constexpr bool BJC = ENV == RL_ENV_BLACKJACK && !UCB;   // compact LDS rows (bj_row)
     const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
+    const uint32_t SL = BJC ? BJ_LDS_STATES : S, SAL = SL * (uint32_t)A, PSAL = (uint32_t)P * SAL;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
@@ -290,7 +320,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint32_t *N = (uint32_t *)(smem + lay.n);
     unsigned long long *T = (unsigned long long *)(smem + lay.t);
     uint16_t *LIST = (uint16_t *)(smem + lay.list);
-    uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSA * 2u));
+    uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSAL * 2u));
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
     double *RCP = (double *)(smem + lay.rcp);
@@ -301,8 +331,19 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // 4 ds_read_b64 per row instead of 2 ds_read_b128 cost more than the bank
     // conflicts they avoid).
     constexpr bool LDS_AM = false;
+    auto lrow = [&](uint32_t s) -> uint32_t {
+        if constexpr (BJC) return bj_row(s);
+        else return s;
+    };
     auto qi = [&](uint32_t tbl, uint32_t s, uint32_t a) -> uint32_t {
-        return LDS_AM ? tbl * SA + a * S + s : tbl * SA + s * (uint32_t)A + a;
+        return LDS_AM ? tbl * SAL + a * SL + lrow(s) : tbl * SAL + lrow(s) * (uint32_t)A + a;
+    };
+    auto dense_of = [&](uint32_t j) -> uint32_t {       // LDS Q index -> HBM [P][S][A] index
+        if constexpr (!LDS_AM && !BJC) return j;
+        const uint32_t tbl = j / SAL, r = j - tbl * SAL;
+        const uint32_t row = LDS_AM ? r % SL : r / (uint32_t)A, a = LDS_AM ? r / SL : r % (uint32_t)A;
+        const uint32_t s = BJC ? bj_dense(row) : row;
+        return tbl * SA + s * (uint32_t)A + a;
     };
     auto lds_of = [&](uint32_t i) -> uint32_t {        // HBM index -> LDS index
         if constexpr (!LDS_AM) return i;
@@ -310,23 +351,25 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         return qi(tbl, r / (uint32_t)A, r % (uint32_t)A);
     };
     if (tid < 8) ACC[tid] = 0ull;
-    for (uint32_t i = tid; i <= nthr; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
-    for (uint32_t i = tid; i < PSA; i += nthr) { Q[lds_of(i)] = (unsigned long long)p.q_base[i]; SUM[i] = 0ull; }
-    for (uint32_t i = tid; i < (PSA + 1u) / 2u; i += nthr) CNT[i] = 0u;
+    for (uint32_t i = tid; i < lay.nrcp; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
+    for (uint32_t j = tid; j < PSAL; j += nthr) { Q[j] = (unsigned long long)p.q_base[dense_of(j)]; SUM[j] = 0ull; }
+    for (uint32_t i = tid; i < (PSAL + 1u) / 2u; i += nthr) CNT[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < PSA; i += nthr) QF8[lds_of(i)] = (uint8_t)p.qf_base[i];
         for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = p.n_base[i];
         if (tid == 0) T[0] = p.t_base[0];
     }
-    if constexpr (ENV != RL_ENV_BLACKJACK)
+    if constexpr (ENV == RL_ENV_TAXI)
+        for (uint32_t i = tid; i < SA; i += nthr) ((uint16_t *)TR)[lds_of(i)] = (uint16_t)p.trans[i];
+    else if constexpr (ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
     if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
         for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
     EnvTables tabs;
-    tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.trans = TR; tabs.trans16 = (const uint16_t *)TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
     tabs.slippery = p.slippery;
@@ -346,6 +389,16 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     };
     // raw rows of state s: table 0 and (double policy) table 1, read once per use
     auto load_rows = [&](uint32_t s, int64_t (&ra)[A], int64_t (&rb)[A]) {
+        if constexpr (BJC) {
+            if (!bj_nonterminal(s)) {                 // read-only terminal row: Q_base
+#pragma unroll
+                for (int i = 0; i < A; ++i) {
+                    ra[i] = p.q_base[s * (uint32_t)A + i];
+                    rb[i] = P == 2 ? p.q_base[SA + s * (uint32_t)A + i] : 0;
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < A; ++i) {
             ra[i] = (int64_t)Q[qi(0, s, i)];
@@ -377,7 +430,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // fits the block, PSA <= nthr): thread i settles entry i every step, so the
     // counter add needs no return value.  Owner form: the step's first
     // contributor (old count 0) settles the entry.
-    const bool sweep = SWEEP == 1 || PSA <= nthr;   // SWEEP == 1: the host checked PSA <= block
+    const bool sweep = SWEEP == 1 || PSAL <= nthr;   // SWEEP == 1: the host checked PSA <= block
     auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
         const uint32_t sh = (idx & 1u) * 16u;
         bool first = false;
@@ -391,9 +444,32 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     auto settle = [&](uint32_t idx) {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
-        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, RCP[n]));
+        const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
+        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
+    };
+    // traces: every action of a visited state receives a contribution
+    // (elegibility_traces_agent.rs:82-96), so the A entries of an LDS row share
+    // one count n — one counter per (table, row) in the CNT region (u32 words):
+    // one atomic per visited state instead of A.  Row sweep when every row has a
+    // thread, else the first contributor of a row lists it.
+    uint32_t *const CNTR = CNT;
+    const bool rsweep = (uint32_t)P * SL <= nthr;
+    auto qi_row = [&](uint32_t tbl, uint32_t row, uint32_t a) -> uint32_t {
+        return LDS_AM ? tbl * SAL + a * SL + row : tbl * SAL + row * (uint32_t)A + a;
+    };
+    auto settle_row = [&](uint32_t rid) {          // rid = tbl*SL + LDS row
+        const uint32_t n = CNTR[rid];
+        const double rc = n < lay.nrcp ? RCP[n] : 1.0 / (double)n;
+        const uint32_t tbl = rid / SL, row = rid - tbl * SL;
+#pragma unroll
+        for (int b = 0; b < A; ++b) {
+            const uint32_t idx = qi_row(tbl, row, (uint32_t)b);
+            Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc));
+            SUM[idx] = 0ull;
+        }
+        CNTR[rid] = 0u;
     };
     // wave-level per-launch counters (scalar registers: ballot popcounts)
     uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
@@ -435,7 +511,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (alive) atomicAdd(&N[qi(0, s2, a2)], 1u);
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
-            __syncthreads();
+            // only expected SARSA's probabilities read the incremented counters in
+            // this step; otherwise the next reader is the next step's selection,
+            // after the end-of-step barrier
+            if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) __syncthreads();
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
@@ -493,7 +572,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
             if (sweep) { if (tid < PSA && CNT16[tid] == 77) settle(tid); }
 #else
-            if (sweep) { if (tid < PSA) settle(tid); }
+            if (sweep) { if (tid < PSAL) settle(tid); }
 #endif
             else if (owner) settle(idx);
         } else {
@@ -504,21 +583,28 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
             const uint32_t nv = train ? tcnt : 0u;
             trace_states += nv;
-            trace_sweep<A>(p, lane, nv, [&](uint32_t o, uint32_t b, double ev) {
+            trace_sweep<A>(p, lane, nv,
+              [&](uint32_t o) {                            // once per visited state: its row count
+                const uint32_t rid = ut * SL + lrow(o);
+                if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+              },
+              [&](uint32_t o, uint32_t b, double ev) {
                 uint32_t fl = 0;
                 int64_t d;
                 if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
                 else d = q_fix_finite(p.lr * (td * ev));
                 const uint32_t idx = qi(ut, o, b);
-                if (contribute(idx, d, 1u, fl) && !sweep) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)idx;
+                if (d) atomicAdd(&SUM[idx], (unsigned long long)d);
+                if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
             });
             if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
-            if (sweep) {
-                if (tid < PSA) settle(tid);
+            if (rsweep) {
+                if (tid < (uint32_t)P * SL) settle_row(tid);
             } else {
                 const uint32_t n_touched = LISTN[0];
-                for (uint32_t i = tid; i < n_touched; i += nthr) settle(LIST[i]);
+                for (uint32_t i = tid; i < n_touched; i += nthr) settle_row(LIST[i]);
                 __syncthreads();
                 if (tid == 0) LISTN[0] = 0u;
             }
@@ -573,8 +659,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // into replica blockIdx % n_rep (folded by k_fold_replicas)
     int64_t *const dl = p.delta_rep + (uint64_t)(blockIdx.x % p.n_rep) * p.delta_words;
     __syncthreads();
-    for (uint32_t i = tid; i < PSA; i += nthr) {
-        const int64_t d = (int64_t)(Q[lds_of(i)] - (unsigned long long)p.q_base[i]);
+    for (uint32_t j = tid; j < PSAL; j += nthr) {
+        const uint32_t i = dense_of(j);
+        const int64_t d = (int64_t)(Q[j] - (unsigned long long)p.q_base[i]);
         if (d) {
             atomicAdd((unsigned long long *)&dl[i], (unsigned long long)d);
             atomicAdd((unsigned long long *)&dl[PSA + i], 1ull);
@@ -638,14 +725,16 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     if (tid < 8) ACC[tid] = 0ull;
-    if constexpr (ENV != RL_ENV_BLACKJACK)
+    if constexpr (ENV == RL_ENV_TAXI)
+        for (uint32_t i = tid; i < SA; i += nthr) ((uint16_t *)TR)[i] = (uint16_t)p.trans[i];
+    else if constexpr (ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
     if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
         for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
     EnvTables tabs;
-    tabs.trans = TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.trans = TR; tabs.trans16 = (const uint16_t *)TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
     tabs.slippery = p.slippery;
@@ -768,7 +857,8 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             // tabular policies, and the oracle's order for the neural one
             trace_visit<A>(p, lane, s, a, tcnt);
             C.trace_states += tcnt;
-            trace_sweep<A>(p, lane, tcnt, [&](uint32_t o, uint32_t b, double ev) { pol_update(ut, o, b, td * ev); });
+            trace_sweep<A>(p, lane, tcnt, [](uint32_t) {},
+                           [&](uint32_t o, uint32_t b, double ev) { pol_update(ut, o, b, td * ev); });
             if (term) tcnt = 0;
         }
         if (P == 2) L.dflag = !L.dflag;                        // after_update
@@ -848,7 +938,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
 
 // ---------------------------------------------------------------- launch table
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int PRIV>
-hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream) {
+hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream, int *occ) {
     const bool instr = p.rec != nullptr || p.elog != nullptr;
     const void *k;
     if constexpr (PRIV) {
@@ -878,6 +968,7 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
+    if (occ) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k, (int)(block.x * block.y * block.z), smem);
     void *args[] = {(void *)&p};
     return hipLaunchKernel(k, grid, block, args, smem, stream);
 }

@@ -117,6 +117,7 @@ SIGNATURES = {
     "rl_agent_launch_train": (C.c_int, [_V]),
     "rl_agent_launch_apply": (C.c_int, [_V]),
     "rl_agent_set_stream": (C.c_int, [_V, _V]),
+    "rl_agent_occupancy": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),
     "rl_agent_set_timing": (C.c_int, [_V, C.c_int32]),
     "rl_agent_get_timing": (C.c_int, [_V, _P(C.c_double), _P(C.c_uint64)]),
     "rl_kat_log": (C.c_int, [C.c_int32, _V, _V, C.c_uint32]),
@@ -410,6 +411,11 @@ class Agent:
 
     def set_stream(self, stream_ptr):
         check(lib().rl_agent_set_stream(self.h, C.c_void_p(stream_ptr)))
+
+    def occupancy(self):
+        g, b, t = C.c_uint32(), C.c_uint64(), C.c_uint32()
+        check(lib().rl_agent_occupancy(self.h, C.byref(g), C.byref(b), C.byref(t)))
+        return {"groups_per_cu": g.value, "lds_bytes": b.value, "block_threads": t.value}
 
     def set_timing(self, on=True):
         check(lib().rl_agent_set_timing(self.h, int(on)))

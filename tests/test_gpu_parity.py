@@ -193,6 +193,18 @@ SHARED_CASES = [
     dict(env="cliff_walking", policy="double", selector="ucb", algo="sarsa", group_size=64),
     dict(env="frozen_lake", agent="traces", policy="double", algo="qlearning", group_size=2),
     dict(env="frozen_lake_edited", map8x8=1, algo="expected_sarsa", group_size=128),
+    # compact Blackjack LDS rows (eps-greedy): terminal rows read from Q_base —
+    # q_default != 0 makes them matter for the TD target and the argmax
+    dict(env="blackjack", algo="sarsa", group_size=300, q_default=0.25),
+    dict(env="blackjack", agent="traces", policy="double", algo="expected_sarsa", group_size=128,
+         q_default=-0.5),
+    dict(env="blackjack", selector="ucb", algo="qlearning", group_size=64),      # dense rows (UCB)
+    # traces: one count per visited row; row list (rows > block) with UCB specials,
+    # and UCB without expected SARSA (no barrier after the counter increments)
+    dict(env="taxi", agent="traces", selector="ucb", algo="expected_sarsa", group_size=256),
+    dict(env="cliff_walking", agent="traces", selector="ucb", algo="sarsa", group_size=64),
+    # owner-form settle with > 64 contributions per entry: 1.0/n by division
+    dict(env="frozen_lake", map8x8=1, algo="sarsa", group_size=200),
 ]
 
 
