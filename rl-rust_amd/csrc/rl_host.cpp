@@ -329,7 +329,9 @@ struct rl_agent {
     // traces
     double *trace = nullptr;
     uint16_t *tlist = nullptr, *slot_of = nullptr;
-    uint32_t *tcnt = nullptr;
+    uint32_t *tcnt = nullptr, *vbits = nullptr;
+    size_t vbits_words = 0;
+    int trace_layout = -1;   // layout_sparse_traces() of the kernel the trace sets were built for
     // Dyna model (private mode)
     uint32_t plan = 0;
     uint32_t *mcnt = nullptr, *mkey = nullptr, *ms2 = nullptr, *mslot = nullptr;
@@ -376,6 +378,17 @@ int agent_select_kernel(rl_agent *a) {
         a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
                                     a->A, (uint32_t)a->eh.cdf.size(), a->block.x);
         if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
+    }
+    if (a->tcnt) {
+        // the trace sets' layout follows the kernel (rl_kparams.h); switching between
+        // the pair and the whole-row layout restarts them (empty sets)
+        const int lay = layout_sparse_traces(a->cfg.agent, a->cfg.selector, a->cfg.algo, a->priv) ? 1 : 0;
+        if (a->trace_layout >= 0 && lay != a->trace_layout) {
+            HIPC(hipSetDevice(a->device));
+            HIPC(hipMemsetAsync(a->tcnt, 0, (size_t)a->L * 4, a->stream));
+            if (a->vbits) HIPC(hipMemsetAsync(a->vbits, 0, a->vbits_words * 4, a->stream));
+        }
+        a->trace_layout = lay;
     }
     return RL_OK;
 }
@@ -763,13 +776,22 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     }
     if (c.agent == RL_AGENT_TRACES) {
         if (a->S > 65535) return bad(fail(RL_E_ARG, "traces need S <= 65535"));
-        const size_t SL = (size_t)a->S * L;
+        // shared mode: room for the pair layout (the selector / algorithm, and so
+        // the layout, may change later: agent_select_kernel)
+        const bool pairs = !a->priv;
+        if (pairs && SA > 32767) return bad(fail(RL_E_ARG, "shared-mode traces need S*A <= 32767"));
+        const size_t SL = (pairs ? SA : (size_t)a->S) * L;   // pair lists are S*A long
         if ((rc = dalloc(&a->trace, SA * L)) || (rc = dalloc(&a->tlist, SL)) || (rc = dalloc(&a->slot_of, SL)) ||
             (rc = dalloc(&a->tcnt, L)))
             return bad(rc);
         if (hipMemset(a->trace, 0, SA * L * 8) != hipSuccess || hipMemset(a->tlist, 0, SL * 2) != hipSuccess ||
             hipMemset(a->slot_of, 0, SL * 2) != hipSuccess || hipMemset(a->tcnt, 0, (size_t)L * 4) != hipSuccess)
             return bad(fail(RL_E_HIP, "memset"));
+        if (pairs) {
+            a->vbits_words = (size_t)((a->S + 31) / 32) * L;
+            if ((rc = dalloc(&a->vbits, a->vbits_words))) return bad(rc);
+            if (hipMemset(a->vbits, 0, a->vbits_words * 4) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+        }
     }
     if (!a->eh.trans.empty() &&
         hipMemcpy(a->trans, a->eh.trans.data(), a->eh.trans.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
@@ -790,7 +812,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
     p.net_w = a->net_w; p.feat = a->feat; p.n_in = a->n_in; p.n_hidden = c.net.hidden; p.n_params = a->n_params;
     p.act1 = c.net.act_hidden; p.act2 = c.net.act_out;
-    p.trace = a->trace; p.tlist = a->tlist; p.slot_of = a->slot_of; p.tcnt = a->tcnt;
+    p.trace = a->trace; p.tlist = a->tlist; p.slot_of = a->slot_of; p.tcnt = a->tcnt; p.vbits = a->vbits;
     p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
     p.fixed_start = a->eh.fixed_start;
     p.slippery = a->eh.slippery;
@@ -818,7 +840,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->q_base); dfree(a->qf_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own);
     dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
-    dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->trans); dfree(a->cdf);
+    dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
     dfree(a->net_w); dfree(a->feat);
@@ -859,6 +881,7 @@ int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats 
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
     if (a->tcnt) HIPC(hipMemsetAsync(a->tcnt, 0, (size_t)a->L * 4, a->stream));   // empty trace sets
+    if (a->vbits) HIPC(hipMemsetAsync(a->vbits, 0, a->vbits_words * 4, a->stream));
     launch_arm_full(a->kp, n_episodes ? RL_MODE_TRAIN : RL_MODE_DONE, 0, 0, 0.0, a->stream);
     HIPC(hipGetLastError());
     if (n_episodes == 0) {

@@ -57,6 +57,11 @@ struct KParams {
     uint16_t *tlist;       // [S][L]
     uint16_t *slot_of;     // [S][L]
     uint32_t *tcnt;        // [L]
+    // shared mode without UCB specials: the same buffers hold visited (state,
+    // action) PAIRS instead — tlist[j] = pair id s*A+a | 0x8000 on the first pair
+    // of its state, slot_of[s*A+a] its slot, trace[j] = E of pair j — plus vbits,
+    // the episode's visited-state bitmap (layout_sparse_traces below)
+    uint32_t *vbits;       // [ceil(S/32)][L]
     // Dyna (InternalModelAgent + RandomModel, private mode): per-lane model as a
     // sparse set in insertion order, entry j = (key = s*A+a, s', r)
     uint32_t plan_steps;
@@ -101,6 +106,13 @@ struct KParams {
 typedef hipError_t (*train_launch_fn)(const KParams &p, dim3 grid, dim3 block, size_t smem,
                                       hipStream_t stream, int *occ);
 
+// shared-mode traces sweep only the visited (state, action) pairs: an action
+// never taken in a visited state has E = 0 and, with a finite td, contributes
+// exactly 0 (it still counts toward its row's n).  UCB + expected SARSA can make
+// td non-finite (0 * inf = NaN flags), so that variant keeps whole rows.
+inline bool layout_sparse_traces(int agent, int sel, int algo, int priv) {
+    return agent == RL_AGENT_TRACES && !priv && !(sel == RL_SEL_UCB && algo == RL_ALGO_EXPECTED_SARSA);
+}
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start,
                          uint32_t nthr);

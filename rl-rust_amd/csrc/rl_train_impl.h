@@ -293,6 +293,70 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
     }
 }
 
+// Shared-mode traces over visited (state, action) PAIRS (layout_sparse_traces):
+// E[s][a] += 1 finds the pair or appends it; the first pair of a state this
+// episode carries 0x8000 (the state joins the visited set: its row is counted
+// once per step, as the reference updates every action of it).
+template <int A>
+__device__ __forceinline__ void pair_visit(const KParams &p, uint64_t lane, uint32_t s, uint32_t a, uint32_t &np) {
+    const uint64_t Ls = p.L;
+    const uint32_t id = s * (uint32_t)A + a;
+    uint32_t j = p.slot_of[(uint64_t)id * Ls + lane];
+    if (j < np && (p.tlist[(uint64_t)j * Ls + lane] & 0x7fffu) == id) {
+        double *e = &p.trace[(uint64_t)j * Ls + lane];
+        *e = *e + 1.0;
+    } else {
+        uint32_t *vw = &p.vbits[(uint64_t)(s >> 5) * Ls + lane];
+        const uint32_t vb = *vw, bit = 1u << (s & 31u);
+        const bool first = (vb & bit) == 0u;
+        if (first) *vw = vb | bit;
+        j = np++;
+        p.tlist[(uint64_t)j * Ls + lane] = (uint16_t)(id | (first ? 0x8000u : 0u));
+        p.slot_of[(uint64_t)id * Ls + lane] = (uint16_t)j;
+        p.trace[(uint64_t)j * Ls + lane] = 1.0;
+    }
+}
+// the sweep over pairs [0, np): fn(pair id, first-of-state, E); E *= gamma*lambda.
+// TC pairs per batch with every load issued before any use.
+template <class Fn>
+__device__ __forceinline__ void pair_sweep(const KParams &p, uint64_t lane, uint32_t np, Fn &&fn) {
+    constexpr uint32_t TC = 8;
+    const uint64_t Ls = p.L;
+    for (uint32_t j0 = 0; j0 < np; j0 += TC) {
+        uint32_t w[TC];
+        double ev[TC];
+#pragma unroll
+        for (uint32_t c = 0; c < TC; ++c) {
+            const uint32_t j = j0 + c < np ? j0 + c : j0;
+            w[c] = p.tlist[(uint64_t)j * Ls + lane];
+            ev[c] = p.trace[(uint64_t)j * Ls + lane];
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < TC; ++c) {
+            if (j0 + c < np) {
+                fn(w[c] & 0x7fffu, (w[c] & 0x8000u) != 0u, ev[c]);
+                p.trace[(uint64_t)(j0 + c) * Ls + lane] = ev[c] * p.gl;
+            }
+        }
+    }
+}
+// the episode ended: the visited-state bitmap is cleared (the pair list by np = 0)
+__device__ __forceinline__ void pair_clear(const KParams &p, uint64_t lane) {
+    const uint32_t nw = (p.S + 31u) >> 5;
+    for (uint32_t w = 0; w < nw; ++w) p.vbits[(uint64_t)w * p.L + lane] = 0u;
+}
+
+// UCB + expected SARSA specials: a step's new NaN/inf flags are ORed into the
+// entry's byte above QF_PENDING while other waves may still read the entry for
+// their TD target; the entry's settle folds them into the visible low bits, so
+// readers see Q_t's flags until the step's barrier (the oracle's df[] applied at
+// step end, rlref.c add_delta).
+constexpr uint32_t QF_MASK = QF_NAN | QF_PINF | QF_NINF, QF_PENDING = 4u;
+__device__ __forceinline__ void fold_flags(uint8_t *QF8, uint32_t idx) {
+    const uint32_t f = QF8[idx];
+    if (f >> QF_PENDING) QF8[idx] = (uint8_t)((f | (f >> QF_PENDING)) & QF_MASK);
+}
+
 // ======================================================================== shared
 // INSTR: step records / episode log compiled in (chosen at launch when either is
 // enabled); the throughput variant carries neither.
@@ -384,7 +448,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 
     // f64 image of entry idx (exact: |raw| <= 2^51)
     auto val = [&](uint32_t idx, int64_t raw) -> double {
-        if constexpr (SPEC) return q_val(raw, QF8[idx]);
+        if constexpr (SPEC) return q_val(raw, QF8[idx] & QF_MASK);
         else return q_val(raw);
     };
     // raw rows of state s: table 0 and (double policy) table 1, read once per use
@@ -437,7 +501,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if (sweep) atomicAdd(&CNT[idx >> 1], n << sh);
         else first = ((atomicAdd(&CNT[idx >> 1], n << sh) >> sh) & 0xffffu) == 0u;
         if (sum) atomicAdd(&SUM[idx], (unsigned long long)sum);
-        if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
+        if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
         return first;
     };
     // owner: Q[idx] += mean of the step's contributions (clamped), clear accumulators
@@ -448,6 +512,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
+        if constexpr (SPEC) fold_flags(QF8, idx);
     };
     // traces: every action of a visited state receives a contribution
     // (elegibility_traces_agent.rs:82-96), so the A entries of an LDS row share
@@ -468,6 +533,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             const uint32_t idx = qi_row(tbl, row, (uint32_t)b);
             Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc));
             SUM[idx] = 0ull;
+            if constexpr (SPEC) fold_flags(QF8, idx);
         }
         CNTR[rid] = 0u;
     };
@@ -580,6 +646,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
             // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
             // own visited set; slot j of all lanes is one coalesced row.
+            constexpr bool PAIRS = !SPEC;                 // layout_sparse_traces
+            if constexpr (PAIRS) {
+                if (train) pair_visit<A>(p, lane, L.s, L.a, tcnt);
+                pair_sweep(p, lane, train ? tcnt : 0u, [&](uint32_t id, bool first, double ev) {
+                    const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
+                    if (first) {                              // the state's row: n += 1
+                        ++trace_states;
+                        const uint32_t rid = ut * SL + lrow(o);
+                        if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                        else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+                    }
+                    const int64_t d = q_fix_finite(p.lr * (td * ev));
+                    if (d) atomicAdd(&SUM[qi(ut, o, b)], (unsigned long long)d);
+                });
+                if (train && term) pair_clear(p, lane);
+            } else {
             if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
             const uint32_t nv = train ? tcnt : 0u;
             trace_states += nv;
@@ -596,8 +678,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 else d = q_fix_finite(p.lr * (td * ev));
                 const uint32_t idx = qi(ut, o, b);
                 if (d) atomicAdd(&SUM[idx], (unsigned long long)d);
-                if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], fl << ((idx & 3u) * 8u)); }
+                if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
             });
+            }
             if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
             if (rsweep) {
