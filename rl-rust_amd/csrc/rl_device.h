@@ -633,7 +633,19 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         return (p * 27u + d) * 2u + ace;
     }
     __device__ static __forceinline__ uint32_t deal(Rng &r) {    // initialize_hands :47-56
-        const uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
+        // four words drawn back to back: when none falls in the rejection zone
+        // (all but ~6e-9 of deals) they are the four sequential draw_card results;
+        // otherwise the deal is redrawn sequentially from the saved state
+        const Rng r0 = r;
+        const uint64_t m0 = (uint64_t)r.next_u32() * 10u, m1 = (uint64_t)r.next_u32() * 10u,
+                       m2 = (uint64_t)r.next_u32() * 10u, m3 = (uint64_t)r.next_u32() * 10u;
+        constexpr uint32_t zone = 0xFFFFFFFFu - 6u;
+        uint32_t p0 = 1u + (uint32_t)(m0 >> 32), p1 = 1u + (uint32_t)(m1 >> 32), d0 = 1u + (uint32_t)(m2 >> 32),
+                 d1 = 1u + (uint32_t)(m3 >> 32);
+        if ((uint32_t)m0 > zone || (uint32_t)m1 > zone || (uint32_t)m2 > zone || (uint32_t)m3 > zone) {
+            r = r0;
+            p0 = draw_card(r); p1 = draw_card(r); d0 = draw_card(r); d1 = draw_card(r);
+        }
         const uint32_t pa = (p0 == 1u || p1 == 1u), da = (d0 == 1u || d1 == 1u);
         return (p0 + p1) | ((d0 + d1) << 8) | (d0 << 16) | (pa << 20) | (da << 21);
     }

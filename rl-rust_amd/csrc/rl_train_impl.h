@@ -444,6 +444,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     LaneRegs L;
     lane_load(p, lane, active, L);
     uint32_t tcnt = 0, trace_states = 0;           // traces: size of the lane's visited set
+    // UCB + expected SARSA: ln(t) once per step.  t changes only by the counter
+    // increments between a step's selection and its probabilities, so the
+    // probabilities' ln(t_{k+1}) is also step k+1's selection value.
+    constexpr bool ESU = UCB && ALGO == RL_ALGO_EXPECTED_SARSA;
+    double lnt_es = 0.0;
+    if constexpr (ESU) lnt_es = rl_log((double)T[0]);
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
 
     // f64 image of entry idx (exact: |raw| <= 2^51)
@@ -480,7 +486,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             return argmax_i64<A>(v);
         } else {                                    // upper_confidence_bound.rs:29-42
             double u[A];
-            const double lnt = rl_log((double)T[0]);
+            const double lnt = ESU ? lnt_es : rl_log((double)T[0]);
 #pragma unroll
             for (int i = 0; i < A; ++i) {
                 double v = val(qi(0, s, i), ra[i]);
@@ -580,7 +586,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // only expected SARSA's probabilities read the incremented counters in
             // this step; otherwise the next reader is the next step's selection,
             // after the end-of-step barrier
-            if constexpr (ALGO == RL_ALGO_EXPECTED_SARSA) __syncthreads();
+            if constexpr (ESU) {
+                __syncthreads();
+                lnt_es = rl_log((double)T[0]);   // this step's probabilities and the next selection
+            }
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
@@ -604,7 +613,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
-                    const double lnt = rl_log((double)T[0]);
+                    const double lnt = lnt_es;
                     double sum = 0.0;
 #pragma unroll
                     for (int i = 0; i < A; ++i) {
