@@ -1850,6 +1850,21 @@ void rlo_batch_get_q(const rlo_batch *b, double *out) {
     }
     for (size_t i = 0; i < nq; ++i) out[i] = q_val(b->q_base[i], b->f_base[i]);
 }
+/* Policy contents set by the caller (rl.h rl_agent_set_q): shared mode stores
+ * each value as fixed point + sticky flags like the merge base, private mode
+ * copies lane tables [L][P][S][A] */
+void rlo_batch_set_q(rlo_batch *b, const double *in) {
+    size_t nq = (size_t)b->P * b->S * b->A;
+    if (b->priv) {
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(b->lanes[i].qd, in + i * nq, nq * sizeof(double));
+        return;
+    }
+    for (size_t i = 0; i < nq; ++i) {
+        uint8_t fl = 0;
+        b->q_base[i] = q_clamp(q_fix(in[i], &fl));
+        b->f_base[i] = fl;
+    }
+}
 void rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out) {
     memcpy(out, b->q_base, sizeof(int64_t) * b->P * b->S * b->A);
 }

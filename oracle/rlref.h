@@ -169,6 +169,7 @@ void   rlo_batch_reset(rlo_batch *b);
  * (NeuralPolicy: Policy::get_values of every state, [L][1][S][A]) */
 void   rlo_batch_get_q(const rlo_batch *b, double *out);
 void   rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out);   /* P*S*A raw fixed point */
+void   rlo_batch_set_q(rlo_batch *b, const double *in);         /* shared P*S*A / private [L][P][S][A] */
 void   rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out);
 void   rlo_batch_get_ucb(const rlo_batch *b, uint32_t *counts, uint64_t *t);
 void   rlo_batch_set_record(rlo_batch *b, int enable);

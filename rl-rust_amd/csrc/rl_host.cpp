@@ -393,6 +393,8 @@ int agent_select_kernel(rl_agent *a) {
     return RL_OK;
 }
 
+void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f);
+
 int agent_reset_policy(rl_agent *a) {
     const size_t PSA = (size_t)a->P * a->S * a->A, SA = (size_t)a->S * a->A;
     if (a->neural) {   // NeuralPolicy::new (generation 0) / Network::reset (src/network.rs:89-93)
@@ -420,8 +422,35 @@ int agent_reset_policy(rl_agent *a) {
         HIPC(hipMemcpyAsync(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice, a->stream));
         HIPC(hipMemcpyAsync(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
+        bj_term_scan(a, q.data(), f.data());
     }
     return RL_OK;
+}
+
+// Blackjack terminal rows (dense obs with player sum > 21 or dealer card > 10:
+// rl_train_impl.h bj_nonterminal) are read-only for the kernels; record whether
+// each table holds one finite value there (KParams::bj_tconst)
+void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f) {
+    a->kp.bj_tconst = 0;
+    if (a->cfg.env.kind != RL_ENV_BLACKJACK || a->priv) return;
+    const size_t SA = (size_t)a->S * a->A;
+    int64_t v[2] = {0, 0};
+    for (uint32_t t = 0; t < a->P; ++t) {
+        bool first = true;
+        for (uint32_t s = 0; s < a->S; ++s) {
+            const uint32_t pl = s / 54u, d = (s >> 1) % 27u;
+            if (pl <= 21u && d <= 10u) continue;
+            for (uint32_t b = 0; b < a->A; ++b) {
+                const size_t i = t * SA + (size_t)s * a->A + b;
+                if (f[i]) return;
+                if (first) { v[t] = q[i]; first = false; }
+                else if (q[i] != v[t]) return;
+            }
+        }
+    }
+    a->kp.bj_tconst = 1;
+    a->kp.bj_traw[0] = v[0];
+    a->kp.bj_traw[1] = v[1];
 }
 
 int agent_reset_selector(rl_agent *a) {
@@ -1028,6 +1057,7 @@ int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
     for (size_t i = 0; i < PSA; ++i) q[i] = q_fix(in[i], f[i]);
     HIPC(hipMemcpy(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice));
+    bj_term_scan(a, q.data(), f.data());
     return RL_OK;
 }
 

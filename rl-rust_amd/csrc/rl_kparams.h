@@ -98,6 +98,12 @@ struct KParams {
     rl_episode_record *elog;   // episode log [elog_cap][L] or null
     uint32_t *elog_cnt;        // [L] episodes logged per lane (ring position = cnt % elog_cap)
     uint32_t elog_cap;
+    // Blackjack compact rows: terminal rows are never written (an update writes
+    // Q[s] of a non-terminal s only), so they keep what reset / set_q stored.
+    // When every terminal entry of table t holds one finite raw value bj_traw[t]
+    // (the host checks at reset / set_q), the kernel uses it instead of a load.
+    int32_t bj_tconst;
+    int64_t bj_traw[2];
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

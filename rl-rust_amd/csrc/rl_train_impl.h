@@ -461,6 +461,14 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     auto load_rows = [&](uint32_t s, int64_t (&ra)[A], int64_t (&rb)[A]) {
         if constexpr (BJC) {
             if (!bj_nonterminal(s)) {                 // read-only terminal row: Q_base
+                if (p.bj_tconst) {                    // one value per table (KParams)
+#pragma unroll
+                    for (int i = 0; i < A; ++i) {
+                        ra[i] = p.bj_traw[0];
+                        rb[i] = P == 2 ? p.bj_traw[1] : 0;
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int i = 0; i < A; ++i) {
                     ra[i] = p.q_base[s * (uint32_t)A + i];
@@ -786,15 +794,21 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 }
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
-// FrozenLake / CliffWalking.  The other variants would spill for no occupancy.
+// FrozenLake / CliffWalking and one-step eps-greedy Blackjack.  The other
+// variants would spill for no occupancy.
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
     train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP>(p);
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
-    return (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_CLIFF_WALKING) && AGENT == RL_AGENT_ONE_STEP &&
-           POLICY == RL_POLICY_TABULAR;
+    return ((ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_CLIFF_WALKING) && AGENT == RL_AGENT_ONE_STEP &&
+            POLICY == RL_POLICY_TABULAR) ||
+           // Blackjack eps-greedy (compact rows: <= 35 KiB per group of 512, four groups
+           // per CU): 67 VGPRs at the default bound left it at 3 groups per CU, i.e. a
+           // second, one-third-full round of workgroups for cfg 5's 1024 groups per GPU
+           (ENV == RL_ENV_BLACKJACK && AGENT == RL_AGENT_ONE_STEP && SEL == RL_SEL_EPS_GREEDY &&
+            POLICY != RL_POLICY_NEURAL);
 }
 
 // ======================================================================== private

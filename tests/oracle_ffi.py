@@ -148,6 +148,7 @@ def lib():
         L.rlo_batch_reset.argtypes = [C.c_void_p]
         L.rlo_batch_get_q.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_get_q_raw.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_set_q.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_get_qflags.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_get_ucb.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.rlo_batch_set_record.argtypes = [C.c_void_p, C.c_int]
@@ -398,6 +399,10 @@ class Batch:
         if self.private:
             return out.reshape(self.L, self.P, self.S, self.A)
         return out.reshape(self.P, self.S, self.A)
+
+    def set_q(self, q):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        lib().rlo_batch_set_q(self.h, q.ctypes.data)
 
     def q_raw(self):
         out = np.zeros(self.P * self.S * self.A, np.int64)

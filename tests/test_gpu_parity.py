@@ -335,12 +335,38 @@ def test_dyna_matches_oracle(rl, oracle, case):
     _assert_q_equal(dev.q(), ref.q())
 
 
+@pytest.mark.parametrize("terminal", ["uniform", "mixed"])
+def test_blackjack_terminal_rows_after_set_q(rl, oracle, terminal):
+    """Compact Blackjack rows read terminal rows from Q_base, or from one
+    per-table constant when set_q / reset left them uniform: both bit-exact."""
+    p = _params(rl, env="blackjack", policy="double", algo="expected_sarsa", n_lanes=1200, group_size=512,
+                sync_every=16, n_episodes_for_decay=40)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    P, S, A = ref.P, ref.S, ref.A
+    rng = np.random.default_rng(11)
+    q = rng.uniform(-1.0, 1.0, (P, S, A))
+    s = np.arange(S)
+    term = ~((s // 54 <= 21) & ((s >> 1) % 27 <= 10))
+    if terminal == "uniform":
+        q[0][term] = 0.375
+        q[1][term] = -0.125
+    dev.set_q(q.reshape(-1))
+    ref.set_q(q.reshape(-1))
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    dev.run(4)
+    ref.run(4)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+
+
 @pytest.mark.parametrize("case", [dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256),
                                   dict(env="cliff_walking", algo="sarsa", group_size=64),
                                   dict(env="taxi", selector="ucb", algo="expected_sarsa", group_size=128),
                                   dict(env="blackjack", policy="double", algo="qlearning", group_size=256),
-                                  dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64)],
-                         ids=["fl-q-o8", "cw-sarsa-o8", "taxi-ucb-es", "bj-double", "cw-traces"])
+                                  dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64),
+                                  dict(env="blackjack", algo="expected_sarsa", group_size=512, q_default=0.25)],
+                         ids=["fl-q-o8", "cw-sarsa-o8", "taxi-ucb-es", "bj-double-o8", "cw-traces", "bj-es-o8"])
 def test_throughput_variant_matches_oracle(rl, oracle, case):
     """The kernels the bench runs (no records, no episode log: the INSTR=false
     and occupancy-8 instantiations): raw Q, UCB counters and stats bit-exact."""
