@@ -149,9 +149,11 @@ def main():
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
 
     def step():
+        if delta is None:                   # one process: launch + merge (fused fold/apply where possible)
+            agent.run(1)
+            return
         agent.launch_train()
-        if delta is not None:
-            dist.all_reduce(delta)          # ΔQ / ΔN / Δt: exact int64 sum over ranks (RCCL)
+        dist.all_reduce(delta)              # ΔQ / ΔN / Δt: exact int64 sum over ranks (RCCL)
         agent.launch_apply()
 
     for _ in range(args.warmup):

@@ -492,7 +492,9 @@ void agent_sync_params(rl_agent *a) {
     p.elog_cap = a->elog_cap;
 }
 
-int launch_train_kernel(rl_agent *a) {
+// merge != nullptr: the caller applies the merge right after this launch (one
+// process, its own delta); *merge = true when the fused fold + apply did it
+int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
     agent_sync_params(a);
     a->kp.episodic = (a->kp.target_episodes || a->kp.eval_at || a->kp.eval_only) ? 1 : 0;
     if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
@@ -512,8 +514,14 @@ int launch_train_kernel(rl_agent *a) {
         HIPC(hipEventRecord(e1, a->stream));
         a->events.emplace_back(e0, e1);
     }
+    if (merge) *merge = false;
     if (!a->priv) {                       // fold the group-delta replicas into the delta
-        launch_fold_replicas(a->kp, a->stream);
+        if (merge && a->delta == a->delta_own && a->cfg.selector != RL_SEL_UCB) {
+            launch_fold_apply(a->kp, a->stream);   // ... and apply it (eps-greedy: sums + counts only)
+            *merge = true;
+        } else {
+            launch_fold_replicas(a->kp, a->stream);
+        }
         HIPC(hipGetLastError());
     }
     a->launches++;
@@ -548,10 +556,10 @@ int run_until_done(rl_agent *a, rl_stats *out) {
             return fail(RL_E_OOM, "recorded stream exceeds 4 GiB: record fewer steps");
         // done-lane counter (slot 5 of every stats replica) is per launch
         HIPC(hipMemset2DAsync(&a->stats_d[5], 64, 0, 8, STATS_REP, a->stream));
-        int rc = launch_train_kernel(a);
+        bool merged = false;
+        int rc = launch_train_kernel(a, &merged);
         if (rc) return rc;
-        rc = launch_apply_kernel(a);
-        if (rc) return rc;
+        if (!merged && (rc = launch_apply_kernel(a))) return rc;
         std::vector<unsigned long long> st(8 * STATS_REP);
         HIPC(hipMemcpyAsync(st.data(), a->stats_d, st.size() * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
@@ -951,10 +959,10 @@ int rl_agent_run(rl_agent *a, uint32_t n) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
     for (uint32_t i = 0; i < n; ++i) {
-        int rc = launch_train_kernel(a);
+        bool merged = false;
+        int rc = launch_train_kernel(a, &merged);
         if (rc) return rc;
-        rc = launch_apply_kernel(a);
-        if (rc) return rc;
+        if (!merged && (rc = launch_apply_kernel(a))) return rc;
     }
     return RL_OK;
 }

@@ -135,6 +135,7 @@ void launch_arm_full(const KParams &p, int32_t mode, uint32_t eval_left, int res
 void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s);
 void launch_apply(const KParams &p, int specials, hipStream_t s);
 void launch_fold_replicas(const KParams &p, hipStream_t s);
+void launch_fold_apply(const KParams &p, hipStream_t s);
 void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);
 void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s);
 void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,

@@ -114,6 +114,50 @@ void launch_fold_replicas(const KParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_fold_replicas, dim3((p.delta_words + 63) / 64), dim3(256), 0, s, p);
 }
 
+// ---------------------------------------------------------------- fused fold + apply
+// One-process merge of an eps-greedy learner (the delta holds [PSA sums][PSA
+// counts] only: no UCB counters, no flag counts): entry i sums its two words over
+// the replicas (4 replica slices per block, as k_fold_replicas), zeroes them and
+// applies k_apply's rule, Q_base[i] += mean.  One launch instead of two.
+__global__ void __launch_bounds__(256) k_fold_apply(KParams p) {
+    __shared__ uint64_t part[2][4][64];
+    const uint32_t PSA = p.P * p.S * p.A;
+    const uint32_t lw = threadIdx.x & 63u, g = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 64u + lw;
+    uint64_t s = 0, c = 0;
+    if (i < PSA) {
+        int64_t *x = p.delta_rep + (uint64_t)g * p.delta_words + i;
+        const uint64_t stride = 4ull * p.delta_words;
+        const uint32_t n = p.n_rep > g ? (p.n_rep - g + 3u) / 4u : 0u;
+#pragma unroll 8
+        for (uint32_t r = 0; r < n; ++r) {
+            s += (uint64_t)x[r * stride];
+            c += (uint64_t)x[r * stride + PSA];
+        }
+#pragma unroll 8
+        for (uint32_t r = 0; r < n; ++r) {
+            x[r * stride] = 0;
+            x[r * stride + PSA] = 0;
+        }
+    }
+    part[0][g][lw] = s;
+    part[1][g][lw] = c;
+    __syncthreads();
+    if (g == 0 && i < PSA) {
+        int64_t *d = p.delta;
+        const int64_t sum = (int64_t)((uint64_t)d[i] + part[0][0][lw] + part[0][1][lw] + part[0][2][lw] + part[0][3][lw]);
+        const int64_t cnt = (int64_t)((uint64_t)d[PSA + i] + part[1][0][lw] + part[1][1][lw] + part[1][2][lw] +
+                                      part[1][3][lw]);
+        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(sum, cnt));
+        d[i] = 0;
+        d[PSA + i] = 0;
+    }
+}
+void launch_fold_apply(const KParams &p, hipStream_t s) {
+    const uint32_t PSA = p.P * p.S * p.A;
+    hipLaunchKernelGGL(k_fold_apply, dim3((PSA + 63) / 64), dim3(256), 0, s, p);
+}
+
 // ---------------------------------------------------------------- merge apply
 // Q_base += Σ_groups ΔQ (already summed by global int64 atomics and, across
 // GPUs, by the caller's all-reduce), then Δ = 0 for the next launch.
