@@ -373,7 +373,18 @@ int agent_select_kernel(rl_agent *a) {
                                      a->A, (uint32_t)a->eh.cdf.size());
     } else {
         const uint32_t g = std::min(a->G, a->L);
-        a->block = dim3(((g + 63) / 64) * 64);
+        // lanes per wave (rl_kparams.h KParams::lpw): 64.  RLAMD_LPW=32/16 spreads a
+        // group over more waves; measured on cfg 4 (2^17 lanes, 2 waves per SIMD at
+        // 64): 32 -> 0.96x, 16 -> 0.58x (VGPRs then allow one group per CU), so
+        // it stays an experiment knob
+        uint32_t lpw = 64;
+        if (const char *e = getenv("RLAMD_LPW")) {
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v == 16 || v == 32 || v == 64) lpw = v;
+        }
+        while ((g + lpw - 1) / lpw > 16) lpw *= 2;   // <= 1024 threads per block
+        a->kp.lpw = lpw;
+        a->block = dim3(((g + lpw - 1) / lpw) * 64);
         a->grid = dim3((a->L + a->G - 1) / a->G);
         a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
                                     a->A, (uint32_t)a->eh.cdf.size(), a->block.x);

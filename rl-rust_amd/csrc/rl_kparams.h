@@ -104,6 +104,10 @@ struct KParams {
     // (the host checks at reset / set_q), the kernel uses it instead of a load.
     int32_t bj_tconst;
     int64_t bj_traw[2];
+    // shared mode: lanes per wavefront (64; 32 / 16 spread a group over more
+    // waves, host knob RLAMD_LPW): lane = group base + wave * lpw + lane-in-wave,
+    // the other wave slots idle
+    uint32_t lpw;
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

@@ -439,8 +439,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     tabs.slippery = p.slippery;
     tabs.S = S;
 
-    const uint64_t lane = (uint64_t)blockIdx.x * p.G + tid;
-    const bool active = tid < p.G && lane < p.L;
+    const uint32_t gl = (tid >> 6) * p.lpw + (tid & 63u);      // lane within the group (KParams::lpw)
+    const uint64_t lane = (uint64_t)blockIdx.x * p.G + gl;
+    const bool active = (tid & 63u) < p.lpw && gl < p.G && lane < p.L;
     LaneRegs L;
     lane_load(p, lane, active, L);
     uint32_t tcnt = 0, trace_states = 0;           // traces: size of the lane's visited set

@@ -335,6 +335,23 @@ def test_dyna_matches_oracle(rl, oracle, case):
     _assert_q_equal(dev.q(), ref.q())
 
 
+@pytest.mark.parametrize("lpw", ["64", "32", "16"])
+@pytest.mark.parametrize("case", [dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=200),
+                                  dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256)],
+                         ids=["cw-traces", "fl-q"])
+def test_lanes_per_wave_mapping(rl, oracle, case, lpw, monkeypatch):
+    """Learner groups spread over more waves (16 / 32 lanes per wave, the
+    layout small grids get) give the same results as 64 lanes per wave."""
+    monkeypatch.setenv("RLAMD_LPW", lpw)
+    p = _params(rl, n_lanes=1000, sync_every=16, n_episodes_for_decay=40, **case)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    dev.run(4)
+    ref.run(4)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+
+
 @pytest.mark.parametrize("terminal", ["uniform", "mixed"])
 def test_blackjack_terminal_rows_after_set_q(rl, oracle, terminal):
     """Compact Blackjack rows read terminal rows from Q_base, or from one
