@@ -386,8 +386,29 @@ int agent_select_kernel(rl_agent *a) {
         a->kp.lpw = lpw;
         a->block = dim3(((g + lpw - 1) / lpw) * 64);
         a->grid = dim3((a->L + a->G - 1) / a->G);
-        a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
-                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x);
+        // pair-trace slots in LDS: what the groups that must be resident together
+        // (groups per CU, at most 2048 threads) leave of the 160 KiB, capped at 64
+        // KiB (cfg 4, 2^17 lanes in groups of 256: 2 per CU -> 25 slots per lane).
+        // Long episodes spill past the slots into HBM, and a wave waits for its
+        // longest list, so more slots pay while occupancy holds: measured on cfg 4
+        // 16 slots 6.6e9, 25 slots 7.0e9 env-steps/s; 1 group per CU 3.9e9.
+        // RLAMD_TRC_KB overrides (experiments)
+        {
+            int ncu = 256;
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, a->device);
+            const uint64_t groups = a->grid.x, per_cu = (groups + (uint64_t)ncu - 1) / (uint64_t)ncu;
+            const uint64_t resident = std::max<uint64_t>(1, std::min<uint64_t>(per_cu, 2048 / a->block.x));
+            const size_t base = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector,
+                                                  a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x, 0);
+            const int64_t room = (int64_t)(160 * 1024 / resident) - (int64_t)base - 1024;
+            a->kp.trc_kb = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(64, room / 1024));
+        }
+        if (const char *e = getenv("RLAMD_TRC_KB")) {
+            const int v = atoi(e);
+            if (v >= 0 && v <= 150) a->kp.trc_kb = (uint32_t)v;
+        }
+        a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo, a->S,
+                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x, a->kp.trc_kb);
         if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
     }
     if (a->tcnt) {

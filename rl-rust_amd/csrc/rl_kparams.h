@@ -59,8 +59,9 @@ struct KParams {
     uint32_t *tcnt;        // [L]
     // shared mode without UCB specials: the same buffers hold visited (state,
     // action) PAIRS instead — tlist[j] = pair id s*A+a | 0x8000 on the first pair
-    // of its state, slot_of[s*A+a] its slot, trace[j] = E of pair j — plus vbits,
-    // the episode's visited-state bitmap (layout_sparse_traces below)
+    // of its state, trace[j] = E of pair j.  During a launch the first slots live
+    // in LDS (rl_train_impl.h PairCache); slot_of[s*A+a] and vbits (the visited
+    // states) index the slots past them (layout_sparse_traces below)
     uint32_t *vbits;       // [ceil(S/32)][L]
     // Dyna (InternalModelAgent + RandomModel, private mode): per-lane model as a
     // sparse set in insertion order, entry j = (key = s*A+a, s', r)
@@ -108,6 +109,7 @@ struct KParams {
     // waves, host knob RLAMD_LPW): lane = group base + wave * lpw + lane-in-wave,
     // the other wave slots idle
     uint32_t lpw;
+    uint32_t trc_kb;       // LDS KiB per learner group for pair-trace slots (rl_train_impl.h smem_layout)
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation
@@ -124,8 +126,8 @@ inline bool layout_sparse_traces(int agent, int sel, int algo, int priv) {
     return agent == RL_AGENT_TRACES && !priv && !(sel == RL_SEL_UCB && algo == RL_ALGO_EXPECTED_SARSA);
 }
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
-size_t shared_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start,
-                         uint32_t nthr);
+size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
+                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb);
 size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
 
 // env-only kernels (batched Env trait) and KAT probes

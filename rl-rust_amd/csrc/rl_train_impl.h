@@ -19,7 +19,8 @@
 namespace rlamd {
 
 struct SmemLayout {
-    uint32_t st, q, sum, cnt, qf, n, t, list, rcp, tr, cdf, total;
+    uint32_t st, q, sum, cnt, qf, n, t, list, rcp, tr, cdf, trc, total;
+    uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -53,9 +54,13 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 //   n/t  UCB counters;  list u16 touched entries + count (traces)
 //   rcp  f64 [nthr+1]   1.0/n for the combination rule (mean_delta)
 //   tr/cdf env tables
+//   trc  pair traces (traces == 2): the first trc_cap slots of every lane's pair
+//        list, ids u16 [cap][nthr] then E f64 [cap][nthr] (column = thread)
 // nthr = the shared kernel's block size; 0 for the private kernel (tables only).
+// traces: 0 none, 1 whole-row visited-state sets, 2 visited-pair sets
 __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int traces, uint32_t S,
-                                                  uint32_t A, uint32_t n_start, uint32_t nthr) {
+                                                  uint32_t A, uint32_t n_start, uint32_t nthr,
+                                                  uint32_t trc_kb = 40u) {
     const int shared_q = nthr != 0;
     SmemLayout l;
     const uint32_t SL = (shared_q && bj_compact(env, ucb)) ? BJ_LDS_STATES : S;   // LDS rows
@@ -76,6 +81,14 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.tr = off; off += env == RL_ENV_TAXI ? align16(SA * 2u) : env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
     l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED || env == RL_ENV_TAXI)
                             ? align16(n_start * 8u) : 0u;
+    // trc_kb KiB per group (KParams::trc_kb), at most S*A slots per lane
+    if (shared_q && traces == 2) {
+        const uint32_t c = trc_kb * 1024u / (nthr * 10u);
+        l.trc_cap = c < S * A ? c : S * A;
+    } else {
+        l.trc_cap = 0u;
+    }
+    l.trc = off; off += l.trc_cap ? align16(l.trc_cap * nthr * 2u) + l.trc_cap * nthr * 8u : 0u;
     l.total = off;
     return l;
 }
@@ -293,57 +306,112 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
     }
 }
 
-// Shared-mode traces over visited (state, action) PAIRS (layout_sparse_traces):
-// E[s][a] += 1 finds the pair or appends it; the first pair of a state this
-// episode carries 0x8000 (the state joins the visited set: its row is counted
-// once per step, as the reference updates every action of it).
+// Shared-mode traces over visited (state, action) PAIRS (layout_sparse_traces).
+// Slot j of a lane's list holds pair id s*A+a (| 0x8000 on the first pair of its
+// state this episode: the state joins the visited set, its row is counted once
+// per step, as the reference updates every action of it) and E of the pair.
+// Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
+// launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
+// [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+struct PairCache {
+    uint16_t *TRI;
+    double *TRE;
+    uint32_t cap, nthr, tid;
+    __device__ __forceinline__ uint32_t ix(uint32_t j) const { return j * nthr + tid; }
+};
+// E[s][a] += 1: find the pair or append it
 template <int A>
-__device__ __forceinline__ void pair_visit(const KParams &p, uint64_t lane, uint32_t s, uint32_t a, uint32_t &np) {
+__device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c, uint64_t lane, uint32_t s,
+                                           uint32_t a, uint32_t &np) {
     const uint64_t Ls = p.L;
-    const uint32_t id = s * (uint32_t)A + a;
-    uint32_t j = p.slot_of[(uint64_t)id * Ls + lane];
-    if (j < np && (p.tlist[(uint64_t)j * Ls + lane] & 0x7fffu) == id) {
-        double *e = &p.trace[(uint64_t)j * Ls + lane];
-        *e = *e + 1.0;
+    const uint32_t id = s * (uint32_t)A + a, id0 = s * (uint32_t)A;
+    const uint32_t nl = np < c.cap ? np : c.cap;
+    uint32_t hit = 0xffffffffu;
+    bool same_state = false;
+    for (uint32_t j = 0; j < nl; ++j) {
+        const uint32_t w = c.TRI[c.ix(j)] & 0x7fffu;
+        if (w == id) hit = j;
+        if (w - id0 < (uint32_t)A) same_state = true;
+    }
+    if (hit != 0xffffffffu) {
+        c.TRE[c.ix(hit)] += 1.0;
+        return;
+    }
+    if (np > c.cap) {                               // overflow part: slot_of lookup
+        const uint32_t j = p.slot_of[(uint64_t)id * Ls + lane];
+        if (j >= c.cap && j < np && (p.tlist[(uint64_t)j * Ls + lane] & 0x7fffu) == id) {
+            double *e = &p.trace[(uint64_t)j * Ls + lane];
+            *e = *e + 1.0;
+            return;
+        }
+    }
+    const uint32_t j = np++;
+    if (j < c.cap) {
+        c.TRI[c.ix(j)] = (uint16_t)(id | (same_state ? 0u : 0x8000u));
+        c.TRE[c.ix(j)] = 1.0;
     } else {
         uint32_t *vw = &p.vbits[(uint64_t)(s >> 5) * Ls + lane];
         const uint32_t vb = *vw, bit = 1u << (s & 31u);
-        const bool first = (vb & bit) == 0u;
-        if (first) *vw = vb | bit;
-        j = np++;
+        const bool first = !same_state && (vb & bit) == 0u;
+        if ((vb & bit) == 0u) *vw = vb | bit;
         p.tlist[(uint64_t)j * Ls + lane] = (uint16_t)(id | (first ? 0x8000u : 0u));
         p.slot_of[(uint64_t)id * Ls + lane] = (uint16_t)j;
         p.trace[(uint64_t)j * Ls + lane] = 1.0;
     }
 }
 // the sweep over pairs [0, np): fn(pair id, first-of-state, E); E *= gamma*lambda.
-// TC pairs per batch with every load issued before any use.
+// LDS slots first, then the HBM slots TC at a time with every load issued first.
 template <class Fn>
-__device__ __forceinline__ void pair_sweep(const KParams &p, uint64_t lane, uint32_t np, Fn &&fn) {
+__device__ __forceinline__ void pair_sweep(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np,
+                                           Fn &&fn) {
+    const uint32_t nl = np < c.cap ? np : c.cap;
+    for (uint32_t j = 0; j < nl; ++j) {
+        const uint32_t w = c.TRI[c.ix(j)];
+        const double ev = c.TRE[c.ix(j)];
+        fn(w & 0x7fffu, (w & 0x8000u) != 0u, ev);
+        c.TRE[c.ix(j)] = ev * p.gl;
+    }
     constexpr uint32_t TC = 8;
     const uint64_t Ls = p.L;
-    for (uint32_t j0 = 0; j0 < np; j0 += TC) {
+    for (uint32_t j0 = c.cap; j0 < np; j0 += TC) {
         uint32_t w[TC];
         double ev[TC];
 #pragma unroll
-        for (uint32_t c = 0; c < TC; ++c) {
-            const uint32_t j = j0 + c < np ? j0 + c : j0;
-            w[c] = p.tlist[(uint64_t)j * Ls + lane];
-            ev[c] = p.trace[(uint64_t)j * Ls + lane];
+        for (uint32_t k = 0; k < TC; ++k) {
+            const uint32_t j = j0 + k < np ? j0 + k : j0;
+            w[k] = p.tlist[(uint64_t)j * Ls + lane];
+            ev[k] = p.trace[(uint64_t)j * Ls + lane];
         }
 #pragma unroll
-        for (uint32_t c = 0; c < TC; ++c) {
-            if (j0 + c < np) {
-                fn(w[c] & 0x7fffu, (w[c] & 0x8000u) != 0u, ev[c]);
-                p.trace[(uint64_t)(j0 + c) * Ls + lane] = ev[c] * p.gl;
+        for (uint32_t k = 0; k < TC; ++k) {
+            if (j0 + k < np) {
+                fn(w[k] & 0x7fffu, (w[k] & 0x8000u) != 0u, ev[k]);
+                p.trace[(uint64_t)(j0 + k) * Ls + lane] = ev[k] * p.gl;
             }
         }
     }
 }
-// the episode ended: the visited-state bitmap is cleared (the pair list by np = 0)
-__device__ __forceinline__ void pair_clear(const KParams &p, uint64_t lane) {
+// the episode ended: the list is emptied by np = 0; the bitmap (set only by
+// HBM-slot appends) is cleared when the list had reached them
+__device__ __forceinline__ void pair_clear(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
+    if (np <= c.cap) return;
     const uint32_t nw = (p.S + 31u) >> 5;
     for (uint32_t w = 0; w < nw; ++w) p.vbits[(uint64_t)w * p.L + lane] = 0u;
+}
+// launch boundaries: LDS slots <-> tlist / trace rows (np persists in p.tcnt)
+__device__ __forceinline__ void pair_cache_load(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
+    const uint32_t nl = np < c.cap ? np : c.cap;
+    for (uint32_t j = 0; j < nl; ++j) {
+        c.TRI[c.ix(j)] = p.tlist[(uint64_t)j * p.L + lane];
+        c.TRE[c.ix(j)] = p.trace[(uint64_t)j * p.L + lane];
+    }
+}
+__device__ __forceinline__ void pair_cache_store(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
+    const uint32_t nl = np < c.cap ? np : c.cap;
+    for (uint32_t j = 0; j < nl; ++j) {
+        p.tlist[(uint64_t)j * p.L + lane] = c.TRI[c.ix(j)];
+        p.trace[(uint64_t)j * p.L + lane] = c.TRE[c.ix(j)];
+    }
 }
 
 // UCB + expected SARSA specials: a step's new NaN/inf flags are ORed into the
@@ -374,7 +442,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES, S, A, p.n_start, nthr);
+    constexpr bool PAIRS = TRACES && !SPEC;            // layout_sparse_traces (rl_kparams.h)
+    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES ? (PAIRS ? 2 : 1) : 0, S, A, p.n_start, nthr, p.trc_kb);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // two u16 counters per word
@@ -452,6 +521,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     double lnt_es = 0.0;
     if constexpr (ESU) lnt_es = rl_log((double)T[0]);
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
+    const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * nthr * 2u)),
+                       lay.trc_cap, nthr, tid};
+    if constexpr (PAIRS) { if (active) pair_cache_load(p, pc, lane, tcnt); }
 
     // f64 image of entry idx (exact: |raw| <= 2^51)
     auto val = [&](uint32_t idx, int64_t raw) -> double {
@@ -664,10 +736,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
             // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
             // own visited set; slot j of all lanes is one coalesced row.
-            constexpr bool PAIRS = !SPEC;                 // layout_sparse_traces
             if constexpr (PAIRS) {
-                if (train) pair_visit<A>(p, lane, L.s, L.a, tcnt);
-                pair_sweep(p, lane, train ? tcnt : 0u, [&](uint32_t id, bool first, double ev) {
+                if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
+                pair_sweep(p, pc, lane, train ? tcnt : 0u, [&](uint32_t id, bool first, double ev) {
                     const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
                     if (first) {                              // the state's row: n += 1
                         ++trace_states;
@@ -678,7 +749,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     const int64_t d = q_fix_finite(p.lr * (td * ev));
                     if (d) atomicAdd(&SUM[qi(ut, o, b)], (unsigned long long)d);
                 });
-                if (train && term) pair_clear(p, lane);
+                if (train && term) pair_clear(p, pc, lane, tcnt);
             } else {
             if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
             const uint32_t nv = train ? tcnt : 0u;
@@ -739,6 +810,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 
     if (active) lane_store(p, lane, L);
     if constexpr (TRACES) { if (active) p.tcnt[lane] = tcnt; }
+    if constexpr (PAIRS) { if (active) pair_cache_store(p, pc, lane, tcnt); }
     {
         const uint32_t c_done = (uint32_t)__popcll(__ballot(active && L.mode == RL_MODE_DONE));
         if ((tid & 63u) == 0) {
@@ -826,7 +898,7 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     const uint32_t S = p.S, SA = S * (uint32_t)A;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES, S, A, p.n_start, 0u);
+    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES ? 1 : 0, S, A, p.n_start, 0u);
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *CDF = (double *)(smem + lay.cdf);
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);

@@ -352,6 +352,21 @@ def test_lanes_per_wave_mapping(rl, oracle, case, lpw, monkeypatch):
     _assert_stats_equal(dev, ref)
 
 
+@pytest.mark.parametrize("trc_kb", ["0", "2", "150"])
+def test_pair_trace_lds_slots(rl, oracle, trc_kb, monkeypatch):
+    """Pair traces with no LDS slots (all in HBM), a few (long episodes spill
+    past them) and every slot in LDS: bit-exact in all three."""
+    monkeypatch.setenv("RLAMD_TRC_KB", trc_kb)
+    p = _params(rl, env="cliff_walking", agent="traces", algo="qlearning", n_lanes=700, group_size=64,
+                sync_every=16, n_episodes_for_decay=40)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    dev.run(5)
+    ref.run(5)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+
+
 @pytest.mark.parametrize("terminal", ["uniform", "mixed"])
 def test_blackjack_terminal_rows_after_set_q(rl, oracle, terminal):
     """Compact Blackjack rows read terminal rows from Q_base, or from one
