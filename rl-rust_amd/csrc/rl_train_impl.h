@@ -328,10 +328,18 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
     const uint32_t nl = np < c.cap ? np : c.cap;
     uint32_t hit = 0xffffffffu;
     bool same_state = false;
-    for (uint32_t j = 0; j < nl; ++j) {
-        const uint32_t w = c.TRI[c.ix(j)] & 0x7fffu;
-        if (w == id) hit = j;
-        if (w - id0 < (uint32_t)A) same_state = true;
+    constexpr uint32_t TB = 8;                      // ids read TB at a time (latency)
+    for (uint32_t j0 = 0; j0 < nl; j0 += TB) {
+        uint32_t w[TB];
+#pragma unroll
+        for (uint32_t k = 0; k < TB; ++k) w[k] = c.TRI[c.ix(j0 + k < nl ? j0 + k : j0)] & 0x7fffu;
+#pragma unroll
+        for (uint32_t k = 0; k < TB; ++k) {
+            if (j0 + k < nl) {
+                if (w[k] == id) hit = j0 + k;
+                if (w[k] - id0 < (uint32_t)A) same_state = true;
+            }
+        }
     }
     if (hit != 0xffffffffu) {
         c.TRE[c.ix(hit)] += 1.0;
@@ -365,11 +373,23 @@ template <class Fn>
 __device__ __forceinline__ void pair_sweep(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np,
                                            Fn &&fn) {
     const uint32_t nl = np < c.cap ? np : c.cap;
-    for (uint32_t j = 0; j < nl; ++j) {
-        const uint32_t w = c.TRI[c.ix(j)];
-        const double ev = c.TRE[c.ix(j)];
-        fn(w & 0x7fffu, (w & 0x8000u) != 0u, ev);
-        c.TRE[c.ix(j)] = ev * p.gl;
+    constexpr uint32_t TL = 4;                      // LDS slots read TL at a time (latency)
+    for (uint32_t j0 = 0; j0 < nl; j0 += TL) {
+        uint32_t w[TL];
+        double ev[TL];
+#pragma unroll
+        for (uint32_t k = 0; k < TL; ++k) {
+            const uint32_t j = j0 + k < nl ? j0 + k : j0;
+            w[k] = c.TRI[c.ix(j)];
+            ev[k] = c.TRE[c.ix(j)];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TL; ++k) {
+            if (j0 + k < nl) {
+                fn(w[k] & 0x7fffu, (w[k] & 0x8000u) != 0u, ev[k]);
+                c.TRE[c.ix(j0 + k)] = ev[k] * p.gl;
+            }
+        }
     }
     constexpr uint32_t TC = 8;
     const uint64_t Ls = p.L;
