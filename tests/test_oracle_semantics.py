@@ -75,6 +75,33 @@ def test_shared_mode_stays_in_range(oracle):
     assert q.min() >= 0.0 and q.max() <= 1.0 + 1e-12 and q.max() > 0.0
 
 
+def test_set_q_fixed_point_and_blackjack_terminal_rows(oracle):
+    """rlo_batch_set_q stores the values as the merge base does (fixed point
+    2^-40, clamp at 2^51, NaN/inf as flags), and Blackjack terminal rows
+    (player > 21 or dealer card > 10) are never written by training."""
+    p = oracle.default_params(env="blackjack", policy="double", algo="qlearning", n_lanes=512, group_size=128,
+                              sync_every=16)
+    b = oracle.Batch(p)
+    P, S, A = b.P, b.S, b.A
+    q = np.random.default_rng(4).uniform(-2.0, 2.0, (P, S, A))
+    q[0, 5, 1] = np.nan
+    q[1, 7, 0] = np.inf
+    q[0, 9, 0] = 5000.0                      # clamped to 2^51 * 2^-40 = 2048
+    b.set_q(q.reshape(-1))
+    raw = b.q_raw()
+    fin = np.isfinite(q) & (np.abs(q) < 2048)
+    assert np.array_equal(raw[fin], np.rint(q[fin] * 2.0**40).astype(np.int64))
+    assert raw[0, 9, 0] == 2**51
+    qq = b.q()
+    assert np.isnan(qq[0, 5, 1]) and qq[1, 7, 0] == np.inf
+    s = np.arange(S)
+    term = ~((s // 54 <= 21) & ((s >> 1) % 27 <= 10))
+    before = raw[:, term, :].copy()
+    b.run(6)
+    assert np.array_equal(b.q_raw()[:, term, :], before)
+    assert not np.array_equal(b.q_raw()[:, ~term, :], raw[:, ~term, :])
+
+
 def test_expected_sarsa_ucb_nan_is_sticky(oracle):
     """UCB + expected SARSA produces NaN Q entries; they never heal."""
     p = oracle.default_params(env="taxi", selector="ucb", algo="expected_sarsa", n_lanes=64,
