@@ -352,6 +352,41 @@ def test_lanes_per_wave_mapping(rl, oracle, case, lpw, monkeypatch):
     _assert_stats_equal(dev, ref)
 
 
+@pytest.mark.parametrize("L,G,kw", [(1, 64, dict(env="frozen_lake", map8x8=1, algo="qlearning")),
+                                    (65, 64, dict(env="taxi", selector="ucb", algo="expected_sarsa")),
+                                    (3, 256, dict(env="cliff_walking", agent="traces", algo="sarsa")),
+                                    (130, 129, dict(env="blackjack", policy="double", algo="sarsa"))],
+                         ids=["fl-L1", "taxi-L65-G64", "cw-traces-L3", "bj-L130-G129"])
+def test_tiny_and_ragged_groups(rl, oracle, L, G, kw):
+    """Edge sizes: one lane, a group larger than the lane count, a last group
+    with a single lane, a group size that is not a multiple of 64."""
+    p = _params(rl, n_lanes=L, group_size=G, sync_every=16, n_episodes_for_decay=40, **kw)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    dev.run(6)
+    ref.run(6)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+
+
+def test_full_size_determinism_and_range(rl):
+    """cfg 2 at full size (2^20 lanes, G 512, K 64): two runs are bit-identical
+    (integer LDS / HBM atomics make the merge order-free) and FrozenLake Q stays
+    in [0, 1]; every lane steps or resets once per synchronous step."""
+    p = _params(rl, env="frozen_lake", map8x8=1, algo="qlearning", n_lanes=1 << 20, group_size=512,
+                sync_every=64)
+    qs = []
+    for _ in range(2):
+        dev = rl.Agent(p)
+        dev.run(3)
+        qs.append(dev.q_raw())
+        st = dev.stats()
+        assert 0 < st["train_steps"] < 3 * 64 * (1 << 20)
+    assert np.array_equal(qs[0], qs[1])
+    q = qs[0].astype(np.float64) * 2.0**-40
+    assert q.min() >= 0.0 and q.max() <= 1.0 and q.max() > 0.0
+
+
 @pytest.mark.parametrize("trc_kb", ["0", "2", "150"])
 def test_pair_trace_lds_slots(rl, oracle, trc_kb, monkeypatch):
     """Pair traces with no LDS slots (all in HBM), a few (long episodes spill
