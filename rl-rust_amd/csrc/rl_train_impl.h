@@ -313,6 +313,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_PAIR_TC
+#define RLAMD_PAIR_TC 8   // HBM pair slots per batch of the sweep (loads issued together)
+#endif
 struct PairCache {
     uint16_t *TRI;
     double *TRE;
@@ -391,7 +394,7 @@ __device__ __forceinline__ void pair_sweep(const KParams &p, const PairCache &c,
             }
         }
     }
-    constexpr uint32_t TC = 8;
+    constexpr uint32_t TC = RLAMD_PAIR_TC;
     const uint64_t Ls = p.L;
     for (uint32_t j0 = c.cap; j0 < np; j0 += TC) {
         uint32_t w[TC];
