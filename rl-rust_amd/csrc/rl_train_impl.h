@@ -313,6 +313,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_COOP_SWEEP
+#define RLAMD_COOP_SWEEP 1   // shared pair traces: wave-cooperative sweep (0: each lane its own list)
+#endif
 #ifndef RLAMD_PAIR_TC
 #define RLAMD_PAIR_TC 8   // HBM pair slots per batch of the sweep (loads issued together)
 #endif
@@ -759,7 +762,58 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
             // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
             // own visited set; slot j of all lanes is one coalesced row.
-            if constexpr (PAIRS) {
+            if constexpr (PAIRS && RLAMD_COOP_SWEEP) {
+                if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
+                // wave-cooperative sweep: the (lane, slot) items of the wave's 64
+                // lanes are dealt out 64 at a time, so a wave takes ceil(sum/64)
+                // rounds instead of its longest list (episode lengths are long-tailed)
+                const uint32_t lid = tid & 63u, wbase = tid & ~63u;
+                const uint32_t npl = train ? tcnt : 0u;
+                uint32_t incl = npl;
+#pragma unroll
+                for (uint32_t o = 1; o < 64; o <<= 1) {
+                    const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+                    if (lid >= o) incl += v;
+                }
+                const uint32_t excl = incl - npl;
+                const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
+                const uint32_t lane_lo = (uint32_t)lane, lane_hi = (uint32_t)(lane >> 32);
+                const uint64_t Ls = p.L;
+                for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
+                    const uint32_t q = q0 + lid;
+                    uint32_t lo = 0;                      // owner: last lane with excl <= q
+#pragma unroll
+                    for (uint32_t st = 32; st; st >>= 1) {
+                        const uint32_t e = (uint32_t)__shfl((int)excl, (int)(lo + st), 64);
+                        if (e <= q) lo += st;
+                    }
+                    const uint32_t j = q - (uint32_t)__shfl((int)excl, (int)lo, 64);
+                    const double td_o = __shfl(td, (int)lo, 64);
+                    const uint32_t ut_o = (uint32_t)__shfl((int)ut, (int)lo, 64);
+                    const uint64_t lane_o = (uint64_t)(uint32_t)__shfl((int)lane_lo, (int)lo, 64) |
+                                            ((uint64_t)(uint32_t)__shfl((int)lane_hi, (int)lo, 64) << 32);
+                    if (q < T) {
+                        const uint32_t col = j * nthr + wbase + lo;
+                        const bool in_lds = j < pc.cap;
+                        const uint32_t w = in_lds ? (uint32_t)pc.TRI[col] : (uint32_t)p.tlist[(uint64_t)j * Ls + lane_o];
+                        const double ev = in_lds ? pc.TRE[col] : p.trace[(uint64_t)j * Ls + lane_o];
+                        const uint32_t id = w & 0x7fffu;
+                        const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
+                        if (w & 0x8000u) {                    // the state's row: n += 1
+                            ++trace_states;
+                            const uint32_t rid = ut_o * SL + lrow(o);
+                            if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                            else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+                        }
+                        const int64_t d = q_fix_finite(p.lr * (td_o * ev));
+                        if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
+                        const double en = ev * p.gl;
+                        if (in_lds) pc.TRE[col] = en;
+                        else p.trace[(uint64_t)j * Ls + lane_o] = en;
+                    }
+                }
+                if (train && term) pair_clear(p, pc, lane, tcnt);
+            } else if constexpr (PAIRS) {
                 if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
                 pair_sweep(p, pc, lane, train ? tcnt : 0u, [&](uint32_t id, bool first, double ev) {
                     const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
