@@ -352,6 +352,43 @@ def test_lanes_per_wave_mapping(rl, oracle, case, lpw, monkeypatch):
     _assert_stats_equal(dev, ref)
 
 
+def _golden():
+    import json, os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "trajectories.json")))
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5"])
+def test_device_matches_golden_trajectories(rl, cfg):
+    """The device against the committed fixtures directly (no oracle in the
+    loop): raw Q, UCB counters and stats after the fixture's launches."""
+    import base64
+    g = _golden()[cfg]
+    dev = rl.Agent(_params(rl, **g["params"]))
+    dev.run(g["launches"])
+    want = np.frombuffer(base64.b64decode(g["q_raw_i64_b64"]), "<i8")
+    assert np.array_equal(dev.q_raw().reshape(-1), want)
+    st, ref = dev.stats(), np.array(g["stats_u64"], np.uint64).view(np.int64)
+    for i, k in STAT_KEYS.items():
+        assert st[k] == int(ref[i]), k
+    if "ucb_t" in g:
+        n, t = dev.ucb()
+        assert t == g["ucb_t"]
+        assert np.array_equal(np.asarray(n).reshape(-1), np.frombuffer(base64.b64decode(g["ucb_n_u32_b64"]), "<u4"))
+
+
+def test_device_matches_golden_cfg1_faithful_loop(rl):
+    """cfg 1 (FrozenLake 4x4, one env, eval interleave on) as one private
+    device agent: the fixture's Q and per-episode histories."""
+    import base64
+    g = _golden()["cfg1"]
+    n, eval_at = g["params"]["n_episodes"], g["params"]["eval_at"]
+    dev = rl.Agent(_params(rl, env="frozen_lake", n_lanes=1, group_size=1, sync_every=64,
+                           n_episodes_for_decay=n))
+    dev.train(n, eval_at)
+    q = dev.q()[0].reshape(-1)
+    assert np.array_equal(q.view(np.uint64), np.frombuffer(base64.b64decode(g["q_f64_b64"]), "<u8"))
+
+
 @pytest.mark.parametrize("L,G,kw", [(1, 64, dict(env="frozen_lake", map8x8=1, algo="qlearning")),
                                     (65, 64, dict(env="taxi", selector="ucb", algo="expected_sarsa")),
                                     (3, 256, dict(env="cliff_walking", agent="traces", algo="sarsa")),

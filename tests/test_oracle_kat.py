@@ -144,3 +144,19 @@ def test_blackjack_obs_ids_injective(oracle):
     L = oracle.lib()
     ids = {L.rlo_blackjack_obs_id(p, d, a) for p in range(32) for d in range(27) for a in range(2)}
     assert len(ids) == 32 * 27 * 2
+
+
+def test_golden_trajectories_match_oracle():
+    """tests/golden/trajectories.json (SURVEY §8(c) ii: cfg 1 faithful loop,
+    cfg 2-5 batched schedule) is what the oracle produces today, bit for bit."""
+    import json
+    import os
+    import sys
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    import make_trajectories
+    want = json.load(open(os.path.join(here, "trajectories.json")))
+    got = json.loads(json.dumps(make_trajectories.generate()))
+    assert got.keys() == want.keys()
+    for k in want:
+        assert got[k] == want[k], k
