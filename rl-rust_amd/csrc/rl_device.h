@@ -682,6 +682,47 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         z = ps | (ds << 8) | (z & 0xffff0000u);
         pos = s2;
     }
+    // reset (doR) or step (doS) of one lane in ONE draw loop, for the learner-group
+    // kernel where a wave holds lanes of both kinds: a reset lane draws P0, P1, D0,
+    // D1, a hit lane one card, a stick lane the dealer's cards while d < 17 — the
+    // same draws in the same order as reset() / step(), but the wave runs
+    // max(draws) iterations instead of the reset block + the hit block + the
+    // dealer loop one after another.
+    __device__ static __forceinline__ void advance(bool doR, bool doS, uint32_t &z, uint32_t a, Rng &r,
+                                                   uint32_t &s2, double &rew, bool &term) {
+        uint32_t ps = z & 0xffu, ds = (z >> 8) & 0xffu, d0 = (z >> 16) & 0xfu, pa = (z >> 20) & 1u,
+                 da = (z >> 21) & 1u;
+        if (doR) { ps = 0u; ds = 0u; d0 = 0u; pa = 0u; da = 0u; }
+        const bool hit = doS && a == 0u, stick = doS && a != 0u;
+        const uint32_t nfix = doR ? 4u : (hit ? 1u : 0u);
+        for (uint32_t i = 0;; ++i) {
+            if (!(i < nfix || (stick && score(ds, da) < 17u))) break;
+            const uint32_t c = draw_card(r);
+            if (doR) {
+                if (i < 2u) { ps += c; pa |= c == 1u ? 1u : 0u; }
+                else { if (i == 2u) d0 = c; ds += c; da |= c == 1u ? 1u : 0u; }
+            } else if (hit) {
+                ps += c;
+            } else {
+                ds += c;
+            }
+        }
+        const uint32_t p = score(ps, pa);
+        if (doR) {
+            z = ps | (ds << 8) | (d0 << 16) | (pa << 20) | (da << 21);
+            s2 = obs(p, d0, pa);                       // reset :105-116
+        } else if (hit) {                              // :121-138
+            if (p > 21u) { s2 = obs(p, score(ds, da), pa); rew = -1.0; term = true; }
+            else { s2 = obs(p, d0, pa); rew = 0.0; term = false; }
+            z = ps | (ds << 8) | (z & 0xffff0000u);
+        } else if (stick) {                            // :139-162
+            const uint32_t d = score(ds, da);
+            s2 = obs(p, d, pa);
+            term = true;
+            rew = d > 21u ? 1.0 : (p > d ? 1.0 : (p < d ? -1.0 : 0.0));
+            z = ps | (ds << 8) | (z & 0xffff0000u);
+        }
+    }
 };
 
 // ------------------------------------------------------------------ selection helpers

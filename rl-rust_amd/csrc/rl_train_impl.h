@@ -313,6 +313,12 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_BJ_ONE_LOOP
+// Blackjack learner groups: reset and step draws in one loop (EnvDev::advance).
+// Parity-green but measured slower on cfg 5 (4.98e10 vs 5.83e10 env-steps/s on
+// the 8-wave kernel), so off
+#define RLAMD_BJ_ONE_LOOP 0
+#endif
 #ifndef RLAMD_COOP_SWEEP
 #define RLAMD_COOP_SWEEP 1   // shared pair traces: wave-cooperative sweep (0: each lane its own list)
 #endif
@@ -671,6 +677,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             fl_advance<ENV == RL_ENV_FROZEN_LAKE_EDITED, SLIP, LDS_AM>(doR, doS, pos, L.z, L.a, L.rng, tabs, s2, r,
                                                                        term);
             L.ready = doR ? true : (term ? false : L.ready);
+        } else if constexpr (ENV == RL_ENV_BLACKJACK && RLAMD_BJ_ONE_LOOP) {
+            E::advance(doR, doS, L.z, L.a, L.rng, s2, r, term);
+            L.ready = doR ? true : (doS && term ? false : L.ready);
         } else if (doR) {
             s2 = E::reset(L.z, L.rng, tabs);
             L.ready = true;
