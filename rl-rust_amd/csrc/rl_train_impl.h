@@ -889,9 +889,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
         }
         c_train += (uint32_t)__popcll(__ballot(train));
-        c_eval += (uint32_t)__popcll(__ballot(doS && !train));
         c_tep += (uint32_t)__popcll(__ballot(tr));
-        c_eep += (uint32_t)__popcll(__ballot(ev));
+        if (p.episodic) {                  // run(): lanes only train, so no eval steps / episodes
+            c_eval += (uint32_t)__popcll(__ballot(doS && !train));
+            c_eep += (uint32_t)__popcll(__ballot(ev));
+        }
     }
 
     if (active) lane_store(p, lane, L);
