@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2
+#define RL_ABI_VERSION 3
 
 enum rl_status {
     RL_OK = 0,
@@ -157,6 +157,10 @@ typedef struct rl_stats {
     uint64_t launches;
     uint64_t trace_states;    /* traces agents: sum over training steps of the visited-set size
                                  swept by the eligibility update (mean = V-bar of SURVEY 8(d)) */
+    /* shared mode (fixed-point Q, value = raw * 2^-40, |raw| <= 2^51): deviations from
+     * the reference's unbounded f64 Q.  0 means every update was exact. */
+    uint64_t q_clamp_hits;    /* entry updates (step settle or merge) clamped at |Q| = 2048 */
+    uint64_t delta_saturations; /* per-lane deltas lr*td saturated at |d| = 2048 */
 } rl_stats;
 
 typedef struct rl_env rl_env;
@@ -221,9 +225,12 @@ int rl_agent_get_q(rl_agent *a, double *out, size_t n);
 int rl_agent_set_q(rl_agent *a, const double *in, size_t n);
 /* shared mode only: raw fixed-point Q (value = raw * 2^-40) */
 int rl_agent_get_q_raw(rl_agent *a, int64_t *out, size_t n);
-/* UCB counters (upper_confidence_bound.rs:11-12): shared [S][A] + t[1];
+/* UCB counters (upper_confidence_bound.rs:11-12, u128 there; u64 here: 2^64
+ * selections of one entry is out of reach): shared [S][A] + t[1];
  * private [n_lanes][S][A] + t[n_lanes] */
-int rl_agent_get_ucb(rl_agent *a, uint32_t *counts, size_t n_counts, uint64_t *t, size_t n_t);
+int rl_agent_get_ucb(rl_agent *a, uint64_t *counts, size_t n_counts, uint64_t *t, size_t n_t);
+/* set the UCB counters (same layout; t >= 1), e.g. to resume a checkpoint */
+int rl_agent_set_ucb(rl_agent *a, const uint64_t *counts, size_t n_counts, const uint64_t *t, size_t n_t);
 /* per-lane epsilon (UniformEpsilonGreed::epsilon, uniform_epsilon_greed.rs:13) */
 int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n);
 /* recording: every launch appends K*n_lanes rl_step_record ([step][lane]) */

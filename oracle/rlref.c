@@ -1304,7 +1304,7 @@ typedef struct {
     uint8_t *visited;
     /* private mode (G == 1): the lane is a whole reference agent */
     double *qd;          /* [P][S][A] f64 */
-    uint32_t *n;         /* [S][A] */
+    uint64_t *n;         /* [S][A] (u128 in the reference) */
     uint64_t t;
     model_t model;       /* InternalModelAgent's RandomModel (private mode) */
 } lane_t;
@@ -1318,13 +1318,13 @@ struct rlo_batch {
     double *qd_g;        /* private mode: current lane's Q */
     int64_t *q_base;     /* [P][S][A] */
     uint8_t *f_base;
-    uint32_t *n_base;    /* [S][A] */
+    uint64_t *n_base;    /* [S][A] UCB counts (u128 in the reference, upper_confidence_bound.rs:11) */
     uint64_t t_base;
     /* current group scratch */
     int64_t *q_g, *dq;
     uint32_t *dc;        /* contributions per entry this step */
     uint8_t *f_g, *df;
-    uint32_t *n_g, *n_g_own;
+    uint64_t *n_g, *n_g_own;
     uint64_t t_g;
     /* merge accumulators */
     int64_t *acc_q, *acc_c; uint8_t *acc_f; int64_t *acc_n; int64_t acc_t;
@@ -1333,11 +1333,12 @@ struct rlo_batch {
     int eval_only;
     int record;
     vec records;
-    uint64_t stats[8];
+    uint64_t stats[16];  /* rl_stats order; 8 = Q clamp hits, 9 = delta saturations */
     uint32_t plan;       /* Dyna planning steps per update (private mode only) */
     netdef net;          /* NeuralPolicy (private mode only) */
     double *feat, *w_g;  /* input features [S][in]; current lane's parameters */
     uint32_t net_gen;
+    uint64_t last_done;  /* lanes DONE at the end of the last launch (rl_stats::done_lanes) */
 };
 
 /* Fixed-point Q (shared mode).  |Q raw| <= 2^51, so every entry converts to
@@ -1347,17 +1348,24 @@ struct rlo_batch {
  * +-2^51 and rounded half-to-even. */
 #define Q_RAW_MAX ((int64_t)1 << 51)   /* |Q| <= 2048 */
 #define D_RAW_MAX 0x1p51
-static int64_t q_fix(double d, uint8_t *flag) {
+static int64_t q_fix_sat(double d, uint8_t *flag, int *sat) {
     if (d != d) { *flag |= QF_NAN; return 0; }
     if (d == INFINITY) { *flag |= QF_PINF; return 0; }
     if (d == -INFINITY) { *flag |= QF_NINF; return 0; }
     double x = d * 0x1p40;
+    if (sat && fabs(x) > D_RAW_MAX) *sat = 1;   /* rl_stats::delta_saturations */
     x = fmax(x, -D_RAW_MAX);
     x = fmin(x, D_RAW_MAX);
     return (int64_t)rint(x);
 }
+static int64_t q_fix(double d, uint8_t *flag) { return q_fix_sat(d, flag, NULL); }
 static inline int64_t q_clamp(int64_t v) {
     return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
+}
+/* the entry update with rl_stats::q_clamp_hits counted */
+static inline int64_t q_clamp_count(rlo_batch *b, int64_t v) {
+    if (v > Q_RAW_MAX || v < -Q_RAW_MAX) b->stats[8]++;
+    return q_clamp(v);
 }
 static inline double q_val(int64_t raw, uint8_t fl) {
     if (fl) {
@@ -1397,7 +1405,7 @@ static uint32_t b_select(rlo_batch *b, lane_t *L, uint32_t s) {
         if (L->eps != 0.0 && uniform01(&L->rng) < L->eps) return uniform_action(&L->rng, b->A);
         return argmax_d(v, b->A);
     }
-    const uint32_t *n = &b->n_g[(size_t)s * b->A];
+    const uint64_t *n = &b->n_g[(size_t)s * b->A];
     double lnt = rlo_log((double)b->t_g);
     double u[MAXA];
     for (uint32_t i = 0; i < b->A; ++i) u[i] = ucb_value(v[i], b->c.ucb_c, lnt, (double)n[i]);
@@ -1440,7 +1448,7 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
     b->dc = (uint32_t *)calloc(nq, 4);
     b->acc_q = (int64_t *)calloc(nq, 8); b->acc_f = (uint8_t *)calloc(nq, 1);
     b->acc_c = (int64_t *)calloc(nq, 8);
-    b->n_base = (uint32_t *)calloc(nsa, 4); b->n_g = b->n_g_own = (uint32_t *)calloc(nsa, 4);
+    b->n_base = (uint64_t *)calloc(nsa, 8); b->n_g = b->n_g_own = (uint64_t *)calloc(nsa, 8);
     b->acc_n = (int64_t *)calloc(nsa, 8);
     b->records.esz = sizeof(rlo_record);
     b->lanes = (lane_t *)calloc(c->n_lanes, sizeof(lane_t));
@@ -1453,7 +1461,7 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
         if (b->feat) b->lanes[i].w = (double *)malloc(sizeof(double) * b->net.np);
         if (b->priv) {
             b->lanes[i].qd = (double *)malloc(nq * sizeof(double));
-            b->lanes[i].n = (uint32_t *)calloc(nsa, sizeof(uint32_t));
+            b->lanes[i].n = (uint64_t *)calloc(nsa, sizeof(uint64_t));
         }
         lane_init(b, &b->lanes[i], c->lane_offset + i);
     }
@@ -1481,7 +1489,7 @@ void rlo_batch_reset(rlo_batch *b) {
     uint8_t fl = 0;
     int64_t d = q_clamp(q_fix(b->c.q_default, &fl));
     for (size_t i = 0; i < nq; ++i) { b->q_base[i] = d; b->f_base[i] = fl; }
-    memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
+    memset(b->n_base, 0, sizeof(uint64_t) * b->S * b->A);
     b->t_base = 1;
     b->net_gen++;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
@@ -1490,7 +1498,7 @@ void rlo_batch_reset(rlo_batch *b) {
         if (L->w) net_init(&b->net, L->w, b->c.seed, b->c.lane_offset + i, b->net_gen);  /* Network::reset */
         if (b->priv) {
             for (size_t k = 0; k < nq; ++k) L->qd[k] = b->c.q_default;
-            memset(L->n, 0, sizeof(uint32_t) * b->S * b->A);
+            memset(L->n, 0, sizeof(uint64_t) * b->S * b->A);
             L->t = 1;
         }
         L->model.cnt = 0;                    /* model.reset (internal_model_agent.rs:79-82) */
@@ -1508,11 +1516,11 @@ int rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps) {
 void rlo_batch_set_selector(rlo_batch *b, int32_t sel) {
     b->c.selector = sel;
     b->specials = b->c.selector == RLO_SEL_UCB && b->c.algo == RLO_ALGO_EXPECTED_SARSA;
-    memset(b->n_base, 0, sizeof(uint32_t) * b->S * b->A);
+    memset(b->n_base, 0, sizeof(uint64_t) * b->S * b->A);
     b->t_base = 1;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
         b->lanes[i].eps = b->c.eps0;
-        if (b->priv) { memset(b->lanes[i].n, 0, sizeof(uint32_t) * b->S * b->A); b->lanes[i].t = 1; }
+        if (b->priv) { memset(b->lanes[i].n, 0, sizeof(uint64_t) * b->S * b->A); b->lanes[i].t = 1; }
     }
 }
 void rlo_batch_set_algo(rlo_batch *b, int32_t algo) {
@@ -1528,7 +1536,9 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
         return;
     }
     uint8_t fl = 0;
-    int64_t d = q_fix(delta, &fl);
+    int sat = 0;
+    int64_t d = q_fix_sat(delta, &fl, &sat);
+    b->stats[9] += (uint64_t)sat;
     b->dq[k] = wrap_add(b->dq[k], d);
     b->dc[k] += 1;
     b->df[k] |= fl;
@@ -1711,7 +1721,7 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     }
     if (b->priv) return;
     for (size_t k = 0; k < nq; ++k) {
-        b->q_g[k] = q_clamp(b->q_g[k] + mean_delta(b->dq[k], b->dc[k]));
+        b->q_g[k] = q_clamp_count(b, b->q_g[k] + mean_delta(b->dq[k], b->dc[k]));
         b->f_g[k] |= b->df[k];
     }
 }
@@ -1755,7 +1765,7 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
         uint32_t lane0 = g * b->G;
         uint32_t nl = b->c.n_lanes - lane0 < b->G ? b->c.n_lanes - lane0 : b->G;
         memcpy(b->q_g, b->q_base, nq * 8); memcpy(b->f_g, b->f_base, nq);
-        memcpy(b->n_g, b->n_base, nsa * 4); b->t_g = b->t_base;
+        memcpy(b->n_g, b->n_base, nsa * 8); b->t_g = b->t_base;
         for (uint32_t k = 0; k < b->K; ++k) {
             group_step(b, lane0, nl, tmp);
             if (tmp) {
@@ -1771,7 +1781,7 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
             if (nf & QF_PINF) fc[nq + i] += 1;
             if (nf & QF_NINF) fc[2 * nq + i] += 1;
         }
-        for (size_t i = 0; i < nsa; ++i) dn[i] += (int64_t)b->n_g[i] - (int64_t)b->n_base[i];
+        for (size_t i = 0; i < nsa; ++i) dn[i] += (int64_t)(b->n_g[i] - b->n_base[i]);
         *dt += (int64_t)(b->t_g - b->t_base);
     }
     free(tmp);
@@ -1783,12 +1793,12 @@ void rlo_batch_apply_delta(rlo_batch *b, const int64_t *delta) {
     const int64_t *dsum = delta, *dcnt = delta + nq, *dn = delta + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
     if (b->priv) { b->stats[6]++; return; }
     for (size_t i = 0; i < nq; ++i) {
-        b->q_base[i] = q_clamp(b->q_base[i] + mean_delta(dsum[i], dcnt[i]));
+        b->q_base[i] = q_clamp_count(b, b->q_base[i] + mean_delta(dsum[i], dcnt[i]));
         if (fc[i]) b->f_base[i] |= QF_NAN;
         if (fc[nq + i]) b->f_base[i] |= QF_PINF;
         if (fc[2 * nq + i]) b->f_base[i] |= QF_NINF;
     }
-    for (size_t i = 0; i < nsa; ++i) b->n_base[i] = (uint32_t)((int64_t)b->n_base[i] + dn[i]);
+    for (size_t i = 0; i < nsa; ++i) b->n_base[i] = b->n_base[i] + (uint64_t)dn[i];
     b->t_base = (uint64_t)((int64_t)b->t_base + *dt);
     b->stats[6]++;
 }
@@ -1800,39 +1810,50 @@ static void run_launch(rlo_batch *b) {
     rlo_batch_apply_delta(b, delta);
     free(delta);
 }
+static uint64_t count_done(const rlo_batch *b) {
+    uint64_t done = 0;
+    for (uint32_t i = 0; i < b->c.n_lanes; ++i) done += b->lanes[i].mode == RLO_MODE_DONE;
+    return done;
+}
 
+/* run(): the device's done-lane slot accumulates over the launches of a run() call */
 void rlo_batch_run(rlo_batch *b, uint32_t n_launches) {
-    for (uint32_t i = 0; i < n_launches; ++i) run_launch(b);
+    for (uint32_t i = 0; i < n_launches; ++i) { run_launch(b); b->last_done += count_done(b); }
 }
 static int all_done(const rlo_batch *b) {
     for (uint32_t i = 0; i < b->c.n_lanes; ++i)
         if (b->lanes[i].mode != RLO_MODE_DONE) return 0;
     return 1;
 }
-uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n, uint64_t eval_at) {
-    b->target_episodes = n; b->eval_at = eval_at; b->eval_only = 0;
+/* every lane starts a new episode with an empty trace set (the reference clears
+ * E on termination, elegibility_traces_agent.rs:98-100, and train()/evaluate()
+ * begin at an episode start); mode set, episode counters 0 (rl.h rl_agent_train) */
+static void arm_lanes(rlo_batch *b, int mode, uint64_t eval_left) {
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
         lane_t *L = &b->lanes[i];
-        L->need_reset = 1; L->train_ep = 0; L->eval_left = 0;
-        L->mode = n ? RLO_MODE_TRAIN : RLO_MODE_DONE;
+        L->need_reset = 1; L->train_ep = 0; L->eval_left = eval_left;
+        L->mode = mode;
         if (L->trace) { memset(L->trace, 0, sizeof(double) * b->S * b->A); memset(L->visited, 0, b->S); L->vcnt = 0; }
     }
+}
+uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n, uint64_t eval_at) {
+    if (n == 0) { arm_lanes(b, RLO_MODE_TRAIN, 0); return 0; }   /* the loop body never runs */
+    b->target_episodes = n; b->eval_at = eval_at; b->eval_only = 0;
+    arm_lanes(b, RLO_MODE_TRAIN, 0);
     uint64_t launches = 0;
-    while (!all_done(b)) { run_launch(b); launches++; }
+    while (!all_done(b)) { run_launch(b); launches++; b->last_done = count_done(b); }
     b->target_episodes = 0; b->eval_at = 0;
+    arm_lanes(b, RLO_MODE_TRAIN, 0);     /* back to training: run() keeps training */
     return launches;
 }
 uint64_t rlo_batch_evaluate(rlo_batch *b, uint64_t n) {
+    if (n == 0) return 0;
     b->eval_only = 1; b->target_episodes = 0; b->eval_at = 0;
-    for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
-        lane_t *L = &b->lanes[i];
-        L->need_reset = 1; L->eval_left = n;
-        L->mode = n ? RLO_MODE_EVAL : RLO_MODE_DONE;
-    }
+    arm_lanes(b, RLO_MODE_EVAL, n);
     uint64_t launches = 0;
-    while (!all_done(b)) { run_launch(b); launches++; }
+    while (!all_done(b)) { run_launch(b); launches++; b->last_done = count_done(b); }
     b->eval_only = 0;
-    for (uint32_t i = 0; i < b->c.n_lanes; ++i) b->lanes[i].mode = RLO_MODE_TRAIN;
+    arm_lanes(b, RLO_MODE_TRAIN, 0);
     return launches;
 }
 void rlo_batch_get_q(const rlo_batch *b, double *out) {
@@ -1871,17 +1892,29 @@ void rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out) {
 void rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out) {
     memcpy(out, b->f_base, (size_t)b->P * b->S * b->A);
 }
-void rlo_batch_get_ucb(const rlo_batch *b, uint32_t *counts, uint64_t *t) {
+void rlo_batch_get_ucb(const rlo_batch *b, uint64_t *counts, uint64_t *t) {
     if (b->priv) {        /* [L][S][A], t[L] */
         size_t nsa = (size_t)b->S * b->A;
         for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
-            memcpy(counts + i * nsa, b->lanes[i].n, nsa * sizeof(uint32_t));
+            memcpy(counts + i * nsa, b->lanes[i].n, nsa * sizeof(uint64_t));
             t[i] = b->lanes[i].t;
         }
         return;
     }
-    memcpy(counts, b->n_base, sizeof(uint32_t) * b->S * b->A);
+    memcpy(counts, b->n_base, sizeof(uint64_t) * b->S * b->A);
     *t = b->t_base;
+}
+void rlo_batch_set_ucb(rlo_batch *b, const uint64_t *counts, const uint64_t *t) {
+    if (b->priv) {
+        size_t nsa = (size_t)b->S * b->A;
+        for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
+            memcpy(b->lanes[i].n, counts + i * nsa, nsa * sizeof(uint64_t));
+            b->lanes[i].t = t[i];
+        }
+        return;
+    }
+    memcpy(b->n_base, counts, sizeof(uint64_t) * b->S * b->A);
+    b->t_base = *t;
 }
 uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap) {
     uint64_t n = b->records.n;
@@ -1890,11 +1923,10 @@ uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap) {
     return n;
 }
 uint64_t rlo_batch_n_records(const rlo_batch *b) { return b->records.n; }
-void rlo_batch_stats(const rlo_batch *b, uint64_t *out8) {
-    memcpy(out8, b->stats, sizeof b->stats);
-    uint64_t done = 0;
-    for (uint32_t i = 0; i < b->c.n_lanes; ++i) done += b->lanes[i].mode == RLO_MODE_DONE;
-    out8[5] = done;
+/* out[16]: rl_stats order (slot 5 = lanes DONE at the end of the last launch) */
+void rlo_batch_stats(const rlo_batch *b, uint64_t *out) {
+    memcpy(out, b->stats, sizeof b->stats);
+    out[5] = b->last_done;
 }
 void rlo_batch_lane_eps(const rlo_batch *b, double *out) {
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) out[i] = b->lanes[i].eps;

@@ -171,12 +171,13 @@ void   rlo_batch_get_q(const rlo_batch *b, double *out);
 void   rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out);   /* P*S*A raw fixed point */
 void   rlo_batch_set_q(rlo_batch *b, const double *in);         /* shared P*S*A / private [L][P][S][A] */
 void   rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out);
-void   rlo_batch_get_ucb(const rlo_batch *b, uint32_t *counts, uint64_t *t);
+void   rlo_batch_get_ucb(const rlo_batch *b, uint64_t *counts, uint64_t *t);
+void   rlo_batch_set_ucb(rlo_batch *b, const uint64_t *counts, const uint64_t *t);
 void   rlo_batch_set_record(rlo_batch *b, int enable);
 /* records of all steps since the last call, laid out [step][lane] */
 uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap);
 uint64_t rlo_batch_n_records(const rlo_batch *b);
-void   rlo_batch_stats(const rlo_batch *b, uint64_t *out8);
+void   rlo_batch_stats(const rlo_batch *b, uint64_t *out16);   /* rl_stats order, see rlref.c */
 void   rlo_batch_lane_eps(const rlo_batch *b, double *out);
 /* NeuralPolicy parameters of every lane, [L][n_params] */
 void   rlo_batch_get_weights(const rlo_batch *b, double *out);

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "rl_kparams.h"
+#include "rl_taxi.h"
 
 #pragma clang fp contract(off)
 
@@ -358,21 +359,30 @@ constexpr int64_t Q_RAW_MAX = (int64_t)1 << 51;
 
 // finite delta -> raw: d*2^40 clamped to +-2^51 then rounded half-to-even; the
 // 1.5*2^52 magic add performs rint and the f64->int64 conversion at once.
-__device__ __forceinline__ int64_t q_fix_finite(double d) {
+// `sat` is set when |d| exceeds the range (rl_stats::delta_saturations).
+__device__ __forceinline__ int64_t q_fix_finite(double d, bool &sat) {
     double x = d * 0x1p40;
+    sat = __builtin_fabs(x) > 0x1p51;
     x = __builtin_fmax(x, -0x1p51);
     x = __builtin_fmin(x, 0x1p51);
     const double y = x + 0x1.8p52;
     return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
 }
 // with sticky non-finite flags (UCB + expected SARSA)
-__device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag) {
+__device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag, bool &sat) {
+    sat = false;
     if (d != d) { flag |= QF_NAN; return 0; }
     if (d == __builtin_inf()) { flag |= QF_PINF; return 0; }
     if (d == -__builtin_inf()) { flag |= QF_NINF; return 0; }
-    return q_fix_finite(d);
+    return q_fix_finite(d, sat);
 }
 __device__ __forceinline__ int64_t q_clamp(int64_t v) {
+    return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
+}
+// clamp with a hit flag (rl_stats::q_clamp_hits): the reference's f64 entry
+// would have left [-2048, 2048] here
+__device__ __forceinline__ int64_t q_clamp(int64_t v, bool &hit) {
+    hit = v > Q_RAW_MAX || v < -Q_RAW_MAX;
     return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
 }
 // (double)raw * 2^-40 for |raw| <= 2^51 in two operations: raw added to the bits
@@ -452,8 +462,6 @@ struct EnvTables {
     int32_t fixed_start;   // >= 0: categorical_sample over the start cdf returns this for every u
     int32_t slippery;      // FrozenLake: the map has stochastic rows (uniform per launch)
     uint32_t S;            // |S|: row stride of an action-major table (AM layout below)
-    const uint16_t *trans16 = nullptr;   // Taxi's 12-bit words as u16 in LDS (training kernels:
-                                         // half the table, two learner groups per CU)
 };
 // Transition-table index of (s, a): state-major trans[s*A + a] (HBM, the private
 // kernel), or action-major trans[a*S + s] (AM: the shared kernel's LDS copy, where
@@ -596,14 +604,18 @@ template <> struct EnvDev<RL_ENV_CLIFF_WALKING> {
     }
 };
 
-// TaxiEnv (src/env/taxi.rs): 500 states x 6 actions, deterministic table.
-// trans[s*6+a]: bits 0-8 next, bits 9-10 reward code {-1,-10,+20}, bit 11 terminated.
+// TaxiEnv (src/env/taxi.rs): 500 states x 6 actions, deterministic.  The
+// transition of (s, a) is computed from the state's digits instead of read from
+// a table (no LDS for it: the learner group's LDS goes to Q and the u64 UCB
+// counters).  taxi_word(s, a) = the table word the host builds (rl_host.cpp
+// build_env checks all 3000 against TaxiEnv::new's loop, taxi.rs:63-112):
+// bits 0-8 next, bits 9-10 reward code {-1,-10,+20}, bit 11 terminated.
 template <> struct EnvDev<RL_ENV_TAXI> {
     static constexpr int A = 6;
     __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &t) {
         const double u = uniform01(r);                 // taxi.rs:136-137
         z = 0;
-        return start_state(t, u);
+        return taxi_start(t.cdf, u);
     }
     template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &,
@@ -611,7 +623,7 @@ template <> struct EnvDev<RL_ENV_TAXI> {
                                                 bool &term) {
         if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :146-149
         z += 1;
-        const uint32_t w = t.trans16 ? (uint32_t)t.trans16[tidx<AM, 6>(t, pos, a)] : t.trans[tidx<AM, 6>(t, pos, a)];
+        const uint32_t w = taxi_word(pos, a);
         s2 = w & 511u;
         const uint32_t rc = (w >> 9) & 3u;
         rew = rc == 0 ? -1.0 : (rc == 1 ? -10.0 : 20.0);

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "rl_kparams.h"
+#include "rl_taxi.h"
 
 using namespace rlamd;
 
@@ -104,6 +105,32 @@ void finish_cdf(EnvHost &e) {
         if (e.cdf[i] > 1.0 - 0x1p-52) e.fixed_start = (int32_t)i;
         break;
     }
+}
+
+// categorical_sample over the cdf (utils.rs:33-43): first i with cdf[i] > u, else 0
+uint32_t linear_sample(const std::vector<double> &cdf, double u) {
+    for (size_t i = 0; i < cdf.size(); ++i)
+        if (cdf[i] > u) return (uint32_t)i;
+    return 0;
+}
+// rl_taxi.h taxi_start (three probes) equals the linear search at every
+// boundary: each c_k and its neighbours, and the u around each k/300 where the
+// first probe moves (between boundaries both are constant).  Checked once.
+bool taxi_start_checked(const EnvHost &e) {
+    static int ok = -1;
+    if (ok >= 0) return ok == 1;
+    std::vector<double> us = {0.0, std::nextafter(1.0, 0.0)};
+    auto around = [&](double x) {
+        double lo = x, hi = x;
+        for (int i = 0; i < 8; ++i) { lo = std::nextafter(lo, 0.0); hi = std::nextafter(hi, 1.0); us.push_back(lo); us.push_back(hi); }
+        us.push_back(x);
+    };
+    for (double c : e.cdf) if (c > 0.0 && c < 1.0) around(c);
+    for (int j = 1; j < 300; ++j) around((double)j / 300.0);
+    ok = 1;
+    for (double u : us)
+        if (u >= 0.0 && u < 1.0 && taxi_start(e.cdf.data(), u) != linear_sample(e.cdf, u)) ok = 0;
+    return ok == 1;
 }
 
 int build_env(const rl_env_config &c, EnvHost &e) {
@@ -205,6 +232,10 @@ int build_env(const rl_env_config &c, EnvHost &e) {
                     }
         for (double &v : e.start) v /= total;   // taxi.rs:117-119
         e.trunc_reward = 0.0;
+        // the kernels compute Taxi's transitions (rl_taxi.h taxi_word): all 3000 must
+        // equal the table built above
+        for (uint32_t i = 0; i < 500u * 6u; ++i)
+            if (taxi_word(i / 6u, i % 6u) != e.trans[i]) return fail(RL_E_STATE, "taxi_word differs from the table");
     } else if (c.kind == RL_ENV_BLACKJACK) {
         e.S = 32 * 27 * 2;   // dense (p_score <= 31, d_score <= 26, p_ace)
         e.A = 2;
@@ -212,6 +243,7 @@ int build_env(const rl_env_config &c, EnvHost &e) {
         return fail(RL_E_ARG, "unknown env kind");
     }
     if (!e.start.empty()) finish_cdf(e);
+    if (c.kind == RL_ENV_TAXI && !taxi_start_checked(e)) return fail(RL_E_STATE, "taxi_start differs from categorical_sample");
     // the device FrozenLake resets assume the built-in maps' single start at 0 (rl_device.h)
     if (e.map && e.fixed_start != 0) return fail(RL_E_ARG, "FrozenLake map must start at position 0");
     return RL_OK;
@@ -317,14 +349,15 @@ struct rl_agent {
     double *epi_reward = nullptr;
     // shared
     int64_t *q_base = nullptr;
-    uint32_t *qf_base = nullptr, *n_base = nullptr;
+    uint32_t *qf_base = nullptr;
+    uint64_t *n_base = nullptr;
     uint64_t *t_base = nullptr;
     int64_t *delta_own = nullptr, *delta = nullptr, *delta_rep = nullptr;
     uint64_t delta_words = 0;
     uint32_t n_rep = 1;
     // private
     double *q_priv = nullptr;
-    uint32_t *n_priv = nullptr;
+    uint64_t *n_priv = nullptr;
     uint64_t *t_priv = nullptr;
     // traces
     double *trace = nullptr;
@@ -440,7 +473,7 @@ int agent_reset_policy(rl_agent *a) {
     } else if (a->priv) {
         launch_fill_f64(a->q_priv, PSA * a->L, a->cfg.q_default, a->stream);
         HIPC(hipGetLastError());
-        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 4, a->stream));
+        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 8, a->stream));
         if (a->t_priv) {
             std::vector<uint64_t> ones(a->L, 1);
             HIPC(hipMemcpyAsync(a->t_priv, ones.data(), a->L * 8, hipMemcpyHostToDevice, a->stream));
@@ -488,14 +521,14 @@ void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f) {
 int agent_reset_selector(rl_agent *a) {
     const size_t SA = (size_t)a->S * a->A;
     if (a->priv) {
-        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 4, a->stream));
+        if (a->n_priv) HIPC(hipMemsetAsync(a->n_priv, 0, SA * a->L * 8, a->stream));
         if (a->t_priv) {
             std::vector<uint64_t> ones(a->L, 1);
             HIPC(hipMemcpyAsync(a->t_priv, ones.data(), a->L * 8, hipMemcpyHostToDevice, a->stream));
             HIPC(hipStreamSynchronize(a->stream));
         }
     } else {
-        HIPC(hipMemsetAsync(a->n_base, 0, SA * 4, a->stream));
+        HIPC(hipMemsetAsync(a->n_base, 0, SA * 8, a->stream));
         const uint64_t one = 1;
         HIPC(hipMemcpyAsync(a->t_base, &one, 8, hipMemcpyHostToDevice, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
@@ -587,16 +620,16 @@ int run_until_done(rl_agent *a, rl_stats *out) {
         if (a->rec_h.size() * sizeof(rl_step_record) > (1ull << 32))
             return fail(RL_E_OOM, "recorded stream exceeds 4 GiB: record fewer steps");
         // done-lane counter (slot 5 of every stats replica) is per launch
-        HIPC(hipMemset2DAsync(&a->stats_d[5], 64, 0, 8, STATS_REP, a->stream));
+        HIPC(hipMemset2DAsync(&a->stats_d[5], STATS_W * 8, 0, 8, STATS_REP, a->stream));
         bool merged = false;
         int rc = launch_train_kernel(a, &merged);
         if (rc) return rc;
         if (!merged && (rc = launch_apply_kernel(a))) return rc;
-        std::vector<unsigned long long> st(8 * STATS_REP);
+        std::vector<unsigned long long> st(STATS_W * STATS_REP);
         HIPC(hipMemcpyAsync(st.data(), a->stats_d, st.size() * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
         unsigned long long done = 0;
-        for (uint32_t r = 0; r < STATS_REP; ++r) done += st[r * 8 + 5];
+        for (uint32_t r = 0; r < STATS_REP; ++r) done += st[r * STATS_W + 5];
         if (const char *dump = getenv("RLAMD_DEBUG_LANES")) {   // diagnostics: raw lane records per launch
             std::vector<uint4> c(a->L);
             HIPC(hipMemcpy(c.data(), a->core, a->L * 16, hipMemcpyDeviceToHost));
@@ -814,7 +847,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     a->stream = a->own_stream;
     const size_t L = a->L, SA = (size_t)a->S * a->A, PSA = a->P * SA;
     if ((rc = dalloc(&a->core, L)) || (rc = dalloc(&a->rng, L)) || (rc = dalloc(&a->aux, L)) ||
-        (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, 8 * STATS_REP)) ||
+        (rc = dalloc(&a->epi_reward, L)) || (rc = dalloc(&a->stats_d, STATS_W * STATS_REP)) ||
         (rc = dalloc(&a->trans, a->eh.trans.size())) || (rc = dalloc(&a->cdf, a->eh.cdf.size())))
         return bad(rc);
     a->neural = c.policy == RL_POLICY_NEURAL;
@@ -868,7 +901,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     if (!a->eh.cdf.empty() &&
         hipMemcpy(a->cdf, a->eh.cdf.data(), a->eh.cdf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         return bad(fail(RL_E_HIP, "table upload"));
-    if (hipMemset(a->stats_d, 0, 64 * STATS_REP) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+    if (hipMemset(a->stats_d, 0, STATS_W * 8 * STATS_REP) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
 
     KParams &p = a->kp;
     p.L = a->L; p.G = a->G; p.K = a->K; p.S = a->S; p.A = a->A; p.P = a->P;
@@ -946,25 +979,46 @@ int rl_agent_reset(rl_agent *a) {
     return agent_reset_selector(a);
 }
 
+namespace {
+// every lane starts a new episode with an empty trace set: the reference clears
+// E on termination (elegibility_traces_agent.rs:98-100) and train()/evaluate()
+// always begin at an episode start, so a lane left mid-episode by run() must not
+// carry its set into the next call
+int clear_traces(rl_agent *a) {
+    if (a->tcnt) HIPC(hipMemsetAsync(a->tcnt, 0, (size_t)a->L * 4, a->stream));
+    if (a->vbits) HIPC(hipMemsetAsync(a->vbits, 0, a->vbits_words * 4, a->stream));
+    return RL_OK;
+}
+// lanes back to TRAIN at an episode start after train()/evaluate() (success or
+// error), so run() keeps training (rl.h: lanes train forever)
+int rearm_train(rl_agent *a) {
+    a->kp.target_episodes = 0;
+    a->kp.eval_at = 0;
+    a->kp.eval_only = 0;
+    launch_arm_full(a->kp, RL_MODE_TRAIN, 0, 0, 0.0, a->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(a->stream));
+    return clear_traces(a);
+}
+}  // namespace
+
 int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
-    if (a->tcnt) HIPC(hipMemsetAsync(a->tcnt, 0, (size_t)a->L * 4, a->stream));   // empty trace sets
-    if (a->vbits) HIPC(hipMemsetAsync(a->vbits, 0, a->vbits_words * 4, a->stream));
-    launch_arm_full(a->kp, n_episodes ? RL_MODE_TRAIN : RL_MODE_DONE, 0, 0, 0.0, a->stream);
+    int rc = clear_traces(a);
+    if (rc) return rc;
+    if (n_episodes == 0) return out ? rl_agent_stats(a, out) : RL_OK;
+    launch_arm_full(a->kp, RL_MODE_TRAIN, 0, 0, 0.0, a->stream);
     HIPC(hipGetLastError());
-    if (n_episodes == 0) {
-        HIPC(hipStreamSynchronize(a->stream));
-        return out ? rl_agent_stats(a, out) : RL_OK;
-    }
     a->kp.target_episodes = n_episodes;
     a->kp.eval_at = eval_at;
     a->kp.eval_div = eval_at ? ~0ull / eval_at + 1ull : 0ull;   // eval_hit() in rl_train_impl.h
     a->kp.eval_only = 0;
-    int rc = run_until_done(a, out);
-    a->kp.target_episodes = 0;
-    a->kp.eval_at = 0;
-    return rc;
+    rc = run_until_done(a, nullptr);
+    const int rc2 = rearm_train(a);
+    if (rc) return rc;
+    if (rc2) return rc2;
+    return out ? rl_agent_stats(a, out) : RL_OK;
 }
 
 int rl_agent_evaluate(rl_agent *a, uint64_t n_episodes, rl_stats *out) {
@@ -972,19 +1026,18 @@ int rl_agent_evaluate(rl_agent *a, uint64_t n_episodes, rl_stats *out) {
     HIPC(hipSetDevice(a->device));
     if (n_episodes == 0) return out ? rl_agent_stats(a, out) : RL_OK;
     if (n_episodes > 0xffffffffull) return fail(RL_E_ARG, "too many evaluation episodes");
+    int rc = clear_traces(a);
+    if (rc) return rc;
     launch_arm_full(a->kp, RL_MODE_EVAL, (uint32_t)n_episodes, 0, 0.0, a->stream);
     HIPC(hipGetLastError());
     a->kp.target_episodes = 0;
     a->kp.eval_at = 0;
     a->kp.eval_only = 1;
-    int rc = run_until_done(a, out);
-    a->kp.eval_only = 0;
+    rc = run_until_done(a, nullptr);
+    const int rc2 = rearm_train(a);   // back to training mode (a new episode on the next call)
     if (rc) return rc;
-    // back to training mode (lanes start a new episode on the next call)
-    launch_arm_full(a->kp, RL_MODE_TRAIN, 0, 0, 0.0, a->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(a->stream));
-    return RL_OK;
+    if (rc2) return rc2;
+    return out ? rl_agent_stats(a, out) : RL_OK;
 }
 
 int rl_agent_run(rl_agent *a, uint32_t n) {
@@ -1009,12 +1062,12 @@ int rl_agent_synchronize(rl_agent *a) {
 int rl_agent_stats(rl_agent *a, rl_stats *out) {
     if (!a || !out) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
-    std::vector<unsigned long long> rep(8 * STATS_REP);
+    std::vector<unsigned long long> rep(STATS_W * STATS_REP);
     HIPC(hipMemcpyAsync(rep.data(), a->stats_d, rep.size() * 8, hipMemcpyDeviceToHost, a->stream));
     HIPC(hipStreamSynchronize(a->stream));
-    unsigned long long s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long s[STATS_W] = {};
     for (uint32_t r = 0; r < STATS_REP; ++r)
-        for (int i = 0; i < 8; ++i) s[i] += rep[r * 8 + i];
+        for (uint32_t i = 0; i < STATS_W; ++i) s[i] += rep[r * STATS_W + i];
     out->train_steps = s[0];
     out->eval_steps = s[1];
     out->train_episodes = s[2];
@@ -1023,6 +1076,8 @@ int rl_agent_stats(rl_agent *a, rl_stats *out) {
     out->done_lanes = s[5];
     out->launches = a->launches;
     out->trace_states = s[7];
+    out->q_clamp_hits = s[ACC_CLAMP];
+    out->delta_saturations = s[ACC_SAT];
     return RL_OK;
 }
 
@@ -1112,14 +1167,14 @@ int rl_agent_get_q_raw(rl_agent *a, int64_t *out, size_t n) {
     return RL_OK;
 }
 
-int rl_agent_get_ucb(rl_agent *a, uint32_t *counts, size_t nc, uint64_t *t, size_t nt) {
+int rl_agent_get_ucb(rl_agent *a, uint64_t *counts, size_t nc, uint64_t *t, size_t nt) {
     if (!a || !counts || !t) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
     const size_t SA = (size_t)a->S * a->A;
     if (a->priv) {
         if (nc < SA * a->L || nt < a->L) return fail(RL_E_ARG, "output too small");
-        std::vector<uint32_t> tmp(SA * a->L);
-        HIPC(hipMemcpyAsync(tmp.data(), a->n_priv, tmp.size() * 4, hipMemcpyDeviceToHost, a->stream));
+        std::vector<uint64_t> tmp(SA * a->L);
+        HIPC(hipMemcpyAsync(tmp.data(), a->n_priv, tmp.size() * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipMemcpyAsync(t, a->t_priv, a->L * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
         for (size_t e = 0; e < SA; ++e)
@@ -1127,8 +1182,30 @@ int rl_agent_get_ucb(rl_agent *a, uint32_t *counts, size_t nc, uint64_t *t, size
         return RL_OK;
     }
     if (nc < SA || nt < 1) return fail(RL_E_ARG, "output too small");
-    HIPC(hipMemcpyAsync(counts, a->n_base, SA * 4, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipMemcpyAsync(counts, a->n_base, SA * 8, hipMemcpyDeviceToHost, a->stream));
     HIPC(hipMemcpyAsync(t, a->t_base, 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+
+int rl_agent_set_ucb(rl_agent *a, const uint64_t *counts, size_t nc, const uint64_t *t, size_t nt) {
+    if (!a || !counts || !t) return fail(RL_E_ARG, "null argument");
+    HIPC(hipSetDevice(a->device));
+    const size_t SA = (size_t)a->S * a->A;
+    const size_t n_t = a->priv ? a->L : 1;
+    if (nc < SA * n_t || nt < n_t) return fail(RL_E_ARG, "input too small");
+    for (size_t i = 0; i < n_t; ++i)
+        if (t[i] == 0) return fail(RL_E_ARG, "UCB t starts at 1 (upper_confidence_bound.rs:20)");
+    if (a->priv) {
+        std::vector<uint64_t> tmp(SA * a->L);   // [L][S][A] -> SoA [entry][lane]
+        for (size_t e = 0; e < SA; ++e)
+            for (size_t l = 0; l < a->L; ++l) tmp[e * a->L + l] = counts[l * SA + e];
+        HIPC(hipMemcpyAsync(a->n_priv, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipMemcpyAsync(a->t_priv, t, a->L * 8, hipMemcpyHostToDevice, a->stream));
+    } else {
+        HIPC(hipMemcpyAsync(a->n_base, counts, SA * 8, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipMemcpyAsync(a->t_base, t, 8, hipMemcpyHostToDevice, a->stream));
+    }
     HIPC(hipStreamSynchronize(a->stream));
     return RL_OK;
 }

@@ -19,6 +19,10 @@ constexpr uint32_t QF_NAN = 1u, QF_PINF = 2u, QF_NINF = 4u;
 // replicas of the u64[8] stats block (same-address atomics from every block
 // serialise; spreading them over replicas removed ~0.3 ms per launch)
 constexpr uint32_t STATS_REP = 64;
+// u64 words per stats replica: rl_stats slots 0-7 (slot 6, launches, is host-side),
+// 8 = q_clamp_hits, 9 = delta_saturations
+constexpr uint32_t STATS_W = 16;
+constexpr uint32_t ACC_CLAMP = 8, ACC_SAT = 9;
 
 // lane core record (uint4, SoA over lanes):
 //   x = s (dense state), y = flags word below, z = env word (curr_step | blackjack hand),
@@ -40,7 +44,7 @@ struct KParams {
     // shared mode
     int64_t *q_base;       // [P][S][A]
     uint32_t *qf_base;     // [P][S][A]
-    uint32_t *n_base;      // [S][A]
+    uint64_t *n_base;      // [S][A] UCB visit counts (u128 in the reference; u64 never wraps in practice)
     uint64_t *t_base;      // [1]
     int64_t *delta;        // [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
     int64_t *delta_rep;    // n_rep replicas of `delta`: group g adds into replica g % n_rep
@@ -48,7 +52,7 @@ struct KParams {
     uint32_t delta_words;
     // private mode (SoA [entry][lane])
     double *q_priv;
-    uint32_t *n_priv;
+    uint64_t *n_priv;      // [S*A][L]
     uint64_t *t_priv;      // [L]
     // eligibility traces, per lane a sparse set of the episode's visited states:
     // tlist[j] = j-th visited state, slot_of[s] = its slot (valid iff
@@ -77,7 +81,7 @@ struct KParams {
     int32_t act1, act2;    // rl_activation of the hidden / output layer
     // env tables
     const uint32_t *trans; // [S][A] packed
-    const double *start_cdf;
+    const double *start_cdf;   // [n_start] running sums (categorical_sample); HBM
     uint32_t n_start;
     int32_t fixed_start;   // >= 0 when the start distribution is a single state
     int32_t slippery;      // FrozenLake with stochastic rows (else the per-step draw is skipped over)
@@ -94,7 +98,7 @@ struct KParams {
     int32_t eval_only;
     int32_t episodic;      // any of target_episodes / eval_at / eval_only set (else the run() fast path)
     // outputs
-    unsigned long long *stats; // rl_stats as u64[8] x STATS_REP replicas (block b adds into b % STATS_REP)
+    unsigned long long *stats; // rl_stats as u64[STATS_W] x STATS_REP replicas (block b adds into b % STATS_REP)
     rl_step_record *rec;       // [K][L] or null
     rl_episode_record *elog;   // episode log [elog_cap][L] or null
     uint32_t *elog_cnt;        // [L] episodes logged per lane (ring position = cnt % elog_cap)

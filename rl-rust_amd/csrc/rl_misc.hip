@@ -149,7 +149,9 @@ __global__ void __launch_bounds__(256) k_fold_apply(KParams p) {
         const int64_t sum = (int64_t)((uint64_t)d[i] + part[0][0][lw] + part[0][1][lw] + part[0][2][lw] + part[0][3][lw]);
         const int64_t cnt = (int64_t)((uint64_t)d[PSA + i] + part[1][0][lw] + part[1][1][lw] + part[1][2][lw] +
                                       part[1][3][lw]);
-        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(sum, cnt));
+        bool hit;
+        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(sum, cnt), hit);
+        if (hit) atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + ACC_CLAMP], 1ull);
         d[i] = 0;
         d[PSA + i] = 0;
     }
@@ -167,7 +169,9 @@ __global__ void k_apply(KParams p, int specials) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int64_t *d = p.delta;
     if (i < PSA) {   // Q_base += mean over the groups (and ranks) that changed the entry
-        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(d[i], d[PSA + i]));
+        bool hit;
+        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(d[i], d[PSA + i]), hit);
+        if (hit) atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + ACC_CLAMP], 1ull);
         d[i] = 0;
         d[PSA + i] = 0;
         if (specials) {
@@ -181,7 +185,7 @@ __global__ void k_apply(KParams p, int specials) {
         }
     }
     if (i < SA) {    // UCB counters are counts: summed
-        p.n_base[i] = (uint32_t)((int64_t)p.n_base[i] + d[2 * PSA + i]);
+        p.n_base[i] = p.n_base[i] + (uint64_t)d[2 * PSA + i];
         d[2 * PSA + i] = 0;
     }
     if (i == 0) {
@@ -200,7 +204,7 @@ __global__ void k_env_reset(KParams p, uint64_t *obs) {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
     EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
-                p.fixed_start, p.slippery};
+                p.fixed_start, p.slippery, p.S};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};
@@ -215,7 +219,7 @@ __global__ void k_env_step(KParams p, const uint32_t *act, uint64_t *obs, double
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= p.L) return;
     EnvTables t{p.trans, p.start_cdf, p.n_start, p.max_steps, p.th1, p.th2, p.th3, p.trunc_reward,
-                p.fixed_start, p.slippery};
+                p.fixed_start, p.slippery, p.S};
     uint4 c = p.core[lane];
     const uint4 r0 = p.rng[lane];
     Rng r{r0.x, r0.y, r0.z, r0.w};

@@ -51,9 +51,10 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 //   sum  int64 [P][S][A]   this step's summed deltas per entry
 //   cnt  u16   [P][S][A]   this step's contributions per entry (u32-word atomics)
 //   qf   u8    [P][S][A]   sticky non-finite flags (UCB + expected SARSA only)
-//   n/t  UCB counters;  list u16 touched entries + count (traces)
+//   n/t  UCB counters (u64 [S][A], u64 t);  list u16 touched entries + count (traces)
 //   rcp  f64 [nthr+1]   1.0/n for the combination rule (mean_delta)
-//   tr/cdf env tables
+//   tr   env transition table (FrozenLake / CliffWalking; Taxi computes its
+//        transitions and reads its start cdf from HBM, Blackjack has none)
 //   trc  pair traces (traces == 2): the first trc_cap slots of every lane's pair
 //        list, ids u16 [cap][nthr] then E f64 [cap][nthr] (column = thread)
 // nthr = the shared kernel's block size; 0 for the private kernel (tables only).
@@ -69,18 +70,20 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     // reach the group size); 64 entries for the owner form (few contributions)
     l.nrcp = !shared_q ? 0u : (PSA <= nthr ? nthr + 1u : (nthr + 1u < 65u ? nthr + 1u : 65u));
     uint32_t off = 0;
-    l.st = off; off += 64u;                       // per-block stats accumulators (u64[8])
+    l.st = off; off += STATS_W * 8u;              // per-block stats accumulators (u64[STATS_W])
     l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.cnt = off; off += shared_q ? align16(((PSA + 1u) / 2u) * 4u) : 0u;
     l.qf = off; off += (shared_q && ucb) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
-    l.n = off; off += (shared_q && ucb) ? align16(SA * 4u) : 0u;
+    l.n = off; off += (shared_q && ucb) ? align16(SA * 8u) : 0u;
     l.t = off; off += (shared_q && ucb) ? 16u : 0u;
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
     l.rcp = off; off += align16(l.nrcp * 8u);
-    l.tr = off; off += env == RL_ENV_TAXI ? align16(SA * 2u) : env != RL_ENV_BLACKJACK ? align16(SA * 4u) : 0u;
-    l.cdf = off; off += (env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED || env == RL_ENV_TAXI)
-                            ? align16(n_start * 8u) : 0u;
+    l.tr = off; off += (env == RL_ENV_TAXI || env == RL_ENV_BLACKJACK) ? 0u : align16(SA * 4u);
+    // start distributions: FrozenLake's maps start at 0 (fixed_start), Taxi probes
+    // the HBM cdf (taxi_start), CliffWalking / Blackjack have none
+    (void)n_start;
+    l.cdf = off;
     // trc_kb KiB per group (KParams::trc_kb), at most S*A slots per lane
     if (shared_q && traces == 2) {
         const uint32_t c = trc_kb * 1024u / (nthr * 10u);
@@ -123,6 +126,7 @@ struct Counters {
     uint32_t trace_states = 0;   // visited-set entries swept by the eligibility update
 };
 
+
 __device__ __forceinline__ void lane_load(const KParams &p, uint64_t lane, bool active, LaneRegs &L) {
     uint4 c = make_uint4(0, 0, 0, 0), r = make_uint4(1, 0, 0, 0), x = make_uint4(0, 0, 0, 0);
     double er = 0.0;
@@ -157,8 +161,8 @@ __device__ __forceinline__ void lane_store(const KParams &p, uint64_t lane, cons
 // Every thread of the block must call these (they contain a barrier).
 __device__ __forceinline__ void flush_block(const KParams &p, unsigned long long *acc) {
     __syncthreads();
-    if (threadIdx.x < 8 && threadIdx.x != 6 && acc[threadIdx.x])
-        atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * 8u + threadIdx.x], acc[threadIdx.x]);
+    if (threadIdx.x < STATS_W && threadIdx.x != 6 && acc[threadIdx.x])
+        atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + threadIdx.x], acc[threadIdx.x]);
 }
 __device__ __forceinline__ void flush_stats(const KParams &p, const LaneRegs &L, const Counters &C,
                                             bool active, unsigned long long *acc) {
@@ -482,12 +486,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
     uint32_t *QF = (uint32_t *)(smem + lay.qf);          // four u8 flag sets per word
     uint8_t *QF8 = (uint8_t *)(smem + lay.qf);
-    uint32_t *N = (uint32_t *)(smem + lay.n);
+    unsigned long long *N = (unsigned long long *)(smem + lay.n);
     unsigned long long *T = (unsigned long long *)(smem + lay.t);
     uint16_t *LIST = (uint16_t *)(smem + lay.list);
     uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSAL * 2u));
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
-    double *CDF = (double *)(smem + lay.cdf);
     double *RCP = (double *)(smem + lay.rcp);
 
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
@@ -515,26 +518,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const uint32_t tbl = i / SA, r = i - tbl * SA;
         return qi(tbl, r / (uint32_t)A, r % (uint32_t)A);
     };
-    if (tid < 8) ACC[tid] = 0ull;
+    if (tid < STATS_W) ACC[tid] = 0ull;
     for (uint32_t i = tid; i < lay.nrcp; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
     for (uint32_t j = tid; j < PSAL; j += nthr) { Q[j] = (unsigned long long)p.q_base[dense_of(j)]; SUM[j] = 0ull; }
     for (uint32_t i = tid; i < (PSAL + 1u) / 2u; i += nthr) CNT[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < PSA; i += nthr) QF8[lds_of(i)] = (uint8_t)p.qf_base[i];
-        for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = p.n_base[i];
+        for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = (unsigned long long)p.n_base[i];
         if (tid == 0) T[0] = p.t_base[0];
     }
-    if constexpr (ENV == RL_ENV_TAXI)
-        for (uint32_t i = tid; i < SA; i += nthr) ((uint16_t *)TR)[lds_of(i)] = (uint16_t)p.trans[i];
-    else if constexpr (ENV != RL_ENV_BLACKJACK)
+    if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
-    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
-        for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
     EnvTables tabs;
-    tabs.trans = TR; tabs.trans16 = (const uint16_t *)TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.trans = TR; tabs.cdf = p.start_cdf; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
     tabs.slippery = p.slippery;
@@ -628,7 +627,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
-        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
+        bool hit;
+        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
+        if (hit) atomicAdd(&ACC[ACC_CLAMP], 1ull);
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
         if constexpr (SPEC) fold_flags(QF8, idx);
@@ -650,7 +651,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
         for (int b = 0; b < A; ++b) {
             const uint32_t idx = qi_row(tbl, row, (uint32_t)b);
-            Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc));
+            bool hit;
+            Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc), hit);
+            if (hit) atomicAdd(&ACC[ACC_CLAMP], 1ull);
             SUM[idx] = 0ull;
             if constexpr (SPEC) fold_flags(QF8, idx);
         }
@@ -696,7 +699,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #endif
         if constexpr (UCB) {
             __syncthreads();
-            if (alive) atomicAdd(&N[qi(0, s2, a2)], 1u);
+            if (alive) atomicAdd(&N[qi(0, s2, a2)], 1ull);
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
             // only expected SARSA's probabilities read the incremented counters in
@@ -751,8 +754,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (train) {
                 uint32_t fl = 0;
                 int64_t dq;
-                if constexpr (SPEC) dq = q_fix(p.lr * td, fl);
-                else dq = q_fix_finite(p.lr * td);
+                bool sat;
+                if constexpr (SPEC) dq = q_fix(p.lr * td, fl, sat);
+                else dq = q_fix_finite(p.lr * td, sat);
+                if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
 #if RLAMD_EXP & 2   // timing experiment: no LDS atomics (results differ)
                 owner = dq == 12345;
 #else
@@ -814,7 +819,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             if (rsweep) atomicAdd(&CNTR[rid], 1u);
                             else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
                         }
-                        const int64_t d = q_fix_finite(p.lr * (td_o * ev));
+                        bool sat;
+                        const int64_t d = q_fix_finite(p.lr * (td_o * ev), sat);
+                        if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
                         if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
                         const double en = ev * p.gl;
                         if (in_lds) pc.TRE[col] = en;
@@ -832,7 +839,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         if (rsweep) atomicAdd(&CNTR[rid], 1u);
                         else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
                     }
-                    const int64_t d = q_fix_finite(p.lr * (td * ev));
+                    bool sat;
+                    const int64_t d = q_fix_finite(p.lr * (td * ev), sat);
+                    if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
                     if (d) atomicAdd(&SUM[qi(ut, o, b)], (unsigned long long)d);
                 });
                 if (train && term) pair_clear(p, pc, lane, tcnt);
@@ -849,8 +858,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
               [&](uint32_t o, uint32_t b, double ev) {
                 uint32_t fl = 0;
                 int64_t d;
-                if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl);
-                else d = q_fix_finite(p.lr * (td * ev));
+                bool sat;
+                if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl, sat);
+                else d = q_fix_finite(p.lr * (td * ev), sat);
+                if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
                 const uint32_t idx = qi(ut, o, b);
                 if (d) atomicAdd(&SUM[idx], (unsigned long long)d);
                 if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
@@ -930,7 +941,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < SA; i += nthr) {
-            const int64_t d = (int64_t)N[lds_of(i)] - (int64_t)p.n_base[i];
+            const int64_t d = (int64_t)(N[lds_of(i)] - (unsigned long long)p.n_base[i]);
             if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + i], (unsigned long long)d);
         }
         if (tid == 0) {
@@ -988,20 +999,15 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES ? 1 : 0, S, A, p.n_start, 0u);
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
-    double *CDF = (double *)(smem + lay.cdf);
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-    if (tid < 8) ACC[tid] = 0ull;
-    if constexpr (ENV == RL_ENV_TAXI)
-        for (uint32_t i = tid; i < SA; i += nthr) ((uint16_t *)TR)[i] = (uint16_t)p.trans[i];
-    else if constexpr (ENV != RL_ENV_BLACKJACK)
+    if (tid < STATS_W) ACC[tid] = 0ull;
+    if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
-    if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED || ENV == RL_ENV_TAXI)
-        for (uint32_t i = tid; i < p.n_start; i += nthr) CDF[i] = p.start_cdf[i];
     __syncthreads();
 
     EnvTables tabs;
-    tabs.trans = TR; tabs.trans16 = (const uint16_t *)TR; tabs.cdf = CDF; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.trans = TR; tabs.cdf = p.start_cdf; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
     tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
     tabs.fixed_start = p.fixed_start;
     tabs.slippery = p.slippery;
@@ -1078,7 +1084,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             for (int i = 0; i < A; ++i)
                 u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)p.n_priv[(uint64_t)(s * A + i) * Ls + lane]);
             const uint32_t a = argmax<A>(u);
-            p.n_priv[(uint64_t)(s * A + a) * Ls + lane] += 1u;
+            p.n_priv[(uint64_t)(s * A + a) * Ls + lane] += 1ull;
             t += 1;
             return a;
         }

@@ -61,7 +61,8 @@ class Stats(C.Structure):
     _fields_ = [("train_steps", C.c_uint64), ("eval_steps", C.c_uint64),
                 ("train_episodes", C.c_uint64), ("eval_episodes", C.c_uint64),
                 ("reward_sum_q16", C.c_int64), ("done_lanes", C.c_uint64),
-                ("launches", C.c_uint64), ("trace_states", C.c_uint64)]
+                ("launches", C.c_uint64), ("trace_states", C.c_uint64),
+                ("q_clamp_hits", C.c_uint64), ("delta_saturations", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -104,6 +105,7 @@ SIGNATURES = {
     "rl_agent_set_q": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_get_q_raw": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_get_ucb": (C.c_int, [_V, _V, C.c_size_t, _V, C.c_size_t]),
+    "rl_agent_set_ucb": (C.c_int, [_V, _V, C.c_size_t, _V, C.c_size_t]),
     "rl_agent_get_epsilon": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_set_recording": (C.c_int, [_V, C.c_int32]),
     "rl_agent_take_records": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64)]),
@@ -331,14 +333,20 @@ class Agent:
 
     def ucb(self):
         if self.private:
-            n = np.zeros(self.L * self.S * self.A, np.uint32)
+            n = np.zeros(self.L * self.S * self.A, np.uint64)
             t = np.zeros(self.L, np.uint64)
             check(lib().rl_agent_get_ucb(self.h, n.ctypes.data, n.size, t.ctypes.data, t.size))
             return n.reshape(self.L, self.S, self.A), t
-        n = np.zeros(self.S * self.A, np.uint32)
+        n = np.zeros(self.S * self.A, np.uint64)
         t = np.zeros(1, np.uint64)
         check(lib().rl_agent_get_ucb(self.h, n.ctypes.data, n.size, t.ctypes.data, 1))
         return n.reshape(self.S, self.A), int(t[0])
+
+    def set_ucb(self, counts, t):
+        """UCB counters (shared [S][A] + t, private [L][S][A] + t[L], u64)"""
+        counts = np.ascontiguousarray(counts, np.uint64).reshape(-1)
+        t = np.ascontiguousarray(np.atleast_1d(t), np.uint64)
+        check(lib().rl_agent_set_ucb(self.h, counts.ctypes.data, counts.size, t.ctypes.data, t.size))
 
     def epsilon(self):
         out = np.zeros(self.L, np.float64)

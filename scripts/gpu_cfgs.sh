@@ -14,5 +14,5 @@ import json; d=json.load(open('gpurun_out/bench_cfg$c.json')); r=d['roofline']
 print('cfg$c', '%.4g'%d['value'], 'kern_ms %.4f'%r['kernel_avg_ms'], 'frac %.3f'%r['frac'])"
 done
 for c in ${PROF_CONFIGS}; do
-  ROUND=r01_cfg$c BENCH_ARGS="--config $c" bash scripts/profile.sh > gpurun_out/profile_cfg$c.log 2>&1 || { rc=$?; echo "profile cfg$c rc=$rc"; exit $rc; }
+  ROUND=${RPFX:-r02}_cfg$c BENCH_ARGS="--config $c ${PROF_ARGS}" bash scripts/profile.sh > gpurun_out/profile_cfg$c.log 2>&1 || { rc=$?; echo "profile cfg$c rc=$rc"; exit $rc; }
 done

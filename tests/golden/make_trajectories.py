@@ -51,11 +51,11 @@ def shared_case(kw):
     b.run(LAUNCHES)
     out = {"params": {**SHARED_SIZE, **kw}, "launches": LAUNCHES,
            "q_raw_i64_b64": b64(b.q_raw().astype("<i8")),
-           "stats_u64": [int(x) for x in b.stats()[:8]],
+           "stats_u64": [int(x) for x in b.stats()[:10]],
            "records_sha256": sha(b.records())}
     if kw.get("selector") == "ucb":
         n, t = b.ucb()
-        out["ucb_n_u32_b64"] = b64(np.asarray(n, "<u4"))
+        out["ucb_n_u64_b64"] = b64(np.asarray(n, "<u8"))
         out["ucb_t"] = int(t)
     return out
 

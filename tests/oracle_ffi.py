@@ -151,6 +151,7 @@ def lib():
         L.rlo_batch_set_q.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_get_qflags.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_get_ucb.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rlo_batch_set_ucb.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.rlo_batch_set_record.argtypes = [C.c_void_p, C.c_int]
         L.rlo_batch_take_records.restype = C.c_uint64
         L.rlo_batch_take_records.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
@@ -416,14 +417,20 @@ class Batch:
 
     def ucb(self):
         if self.private:
-            n = np.zeros(self.L * self.S * self.A, np.uint32)
+            n = np.zeros(self.L * self.S * self.A, np.uint64)
             t = np.zeros(self.L, np.uint64)
             lib().rlo_batch_get_ucb(self.h, n.ctypes.data, t.ctypes.data)
             return n.reshape(self.L, self.S, self.A), t
-        n = np.zeros(self.S * self.A, np.uint32)
+        n = np.zeros(self.S * self.A, np.uint64)
         t = C.c_uint64()
         lib().rlo_batch_get_ucb(self.h, n.ctypes.data, C.byref(t))
         return n.reshape(self.S, self.A), t.value
+
+    def set_ucb(self, counts, t):
+        """UCB counters: shared [S][A] + t, private [L][S][A] + t[L] (u64)"""
+        counts = np.ascontiguousarray(counts, np.uint64)
+        t = np.ascontiguousarray(np.atleast_1d(t), np.uint64)
+        lib().rlo_batch_set_ucb(self.h, counts.ctypes.data, t.ctypes.data)
 
     def records(self):
         """[n_steps, n_lanes] records since the last call (clears the buffer)."""
@@ -444,7 +451,8 @@ class Batch:
         lib().rlo_batch_apply_delta(self.h, np.ascontiguousarray(delta, np.int64).ctypes.data)
 
     def stats(self):
-        out = np.zeros(8, np.uint64)
+        """rl_stats order: 0 train_steps .. 7 trace_states, 8 q_clamp_hits, 9 delta_saturations"""
+        out = np.zeros(16, np.uint64)
         lib().rlo_batch_stats(self.h, out.ctypes.data)
         return out
 

@@ -174,7 +174,7 @@ def test_private_mode_matches_reference_loop(rl, oracle, case):
 
 
 STAT_KEYS = {0: "train_steps", 1: "eval_steps", 2: "train_episodes", 3: "eval_episodes",
-             4: "reward_sum_q16", 7: "trace_states"}
+             4: "reward_sum_q16", 7: "trace_states", 8: "q_clamp_hits", 9: "delta_saturations"}
 
 
 def _assert_stats_equal(dev, ref):
@@ -373,7 +373,7 @@ def test_device_matches_golden_trajectories(rl, cfg):
     if "ucb_t" in g:
         n, t = dev.ucb()
         assert t == g["ucb_t"]
-        assert np.array_equal(np.asarray(n).reshape(-1), np.frombuffer(base64.b64decode(g["ucb_n_u32_b64"]), "<u4"))
+        assert np.array_equal(np.asarray(n).reshape(-1), np.frombuffer(base64.b64decode(g["ucb_n_u64_b64"]), "<u8"))
 
 
 def test_device_matches_golden_cfg1_faithful_loop(rl):

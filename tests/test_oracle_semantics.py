@@ -209,3 +209,28 @@ def test_gen_range_index_kat(oracle):
     assert rej.value == 1
     # range 4 (power of two): zone = 2^64 - 1, never rejects; index = top 2 bits
     assert L.rlo_gen_index_u64(0xC000000000000000, 4, __import__("ctypes").byref(rej)) == 3 and rej.value == 0
+
+
+def test_ucb_counters_are_u64_and_monotone(oracle):
+    """UCB counts (u128 in upper_confidence_bound.rs:11-12) never wrap: seeded
+    just below 2^32 they only grow, and t grows by one per selection."""
+    p = oracle.default_params(env="taxi", selector="ucb", algo="qlearning", n_lanes=256, group_size=64,
+                              sync_every=16)
+    b = oracle.Batch(p)
+    n0 = np.full((b.S, b.A), (1 << 32) - 3, np.uint64)
+    b.set_ucb(n0, 1 << 40)
+    b.run(2)
+    n, t = b.ucb()
+    assert n.dtype == np.uint64 and (n >= n0).all() and (n > (1 << 32)).any()
+    # every live lane selects once per synchronous step (reset or step)
+    assert t - (1 << 40) == int((n - n0).sum()) == 2 * 16 * 256
+
+
+def test_train_then_run_keeps_training_oracle(oracle):
+    p = oracle.default_params(env="cliff_walking", agent="traces", algo="sarsa", n_lanes=64, group_size=32,
+                              sync_every=16, n_episodes_for_decay=40)
+    b = oracle.Batch(p)
+    b.train_episodes(3, 0)
+    s0 = int(b.stats()[0])
+    b.run(2)
+    assert int(b.stats()[0]) > s0
