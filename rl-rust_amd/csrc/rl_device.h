@@ -349,6 +349,37 @@ __device__ __forceinline__ double ucb_value(double q, double c, double lnt, doub
     return q + c * __builtin_sqrt(lnt / (n + MIN_POSITIVE));
 }
 
+// The UCB values of a row without the division and square root where IEEE
+// arithmetic fixes the result (the bench regime of Expected SARSA +
+// UCB is almost all such rows):
+//   n_i == 0: lnt / (0 + MIN_POSITIVE) is exactly lnt * 2^1022 (a power-of-two
+//             quotient; it overflows to +inf from t = 55), so u_i = v_i + b0 with
+//             b0 = c * sqrt(lnt * 2^1022) shared by the row;
+//   n_i >= 1 and v_i non-finite: the bonus c * sqrt(lnt / n) is finite (lnt <=
+//             ln 2^64 < 45, |c| < 2^1020), u_i = v_i.
+// Returns the mask of entries still needing ucb_value (u[i] = 0 for them).
+template <int A>
+__device__ __forceinline__ uint32_t ucb_known(const double (&v)[A], const uint64_t (&n)[A], double c, double lnt,
+                                              double (&u)[A]) {
+    const double b0 = c * __builtin_sqrt(lnt * 0x1p1022);
+    const bool c_fin = __builtin_fabs(c) < 0x1p1020;
+    uint32_t need = 0;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+        const bool z = n[i] == 0ull, nf = !__builtin_isfinite(v[i]) && c_fin;
+        u[i] = z ? v[i] + b0 : (nf ? v[i] : 0.0);
+        need |= (!z && !nf) ? (1u << i) : 0u;
+    }
+    return need;
+}
+template <int A>
+__device__ __forceinline__ void ucb_fill(const double (&v)[A], const uint64_t (&n)[A], double c, double lnt,
+                                         uint32_t need, double (&u)[A]) {
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+        if ((need >> i) & 1u) u[i] = ucb_value(v[i], c, lnt, (double)n[i]);
+}
+
 // ------------------------------------------------------------------ fixed-point Q
 // Shared-mode Q entries are int64 fixed point, value = raw * 2^-40, clamped to
 // |raw| <= 2^51 (|Q| <= 2048; |r| <= 100 and gamma = 0.95 keep every reference

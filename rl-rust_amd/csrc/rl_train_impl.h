@@ -597,14 +597,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             for (int i = 0; i < A; ++i) v[i] = P == 2 ? ra[i] + rb[i] : ra[i];
             return argmax_i64<A>(v);
         } else {                                    // upper_confidence_bound.rs:29-42
-            double u[A];
+            double u[A], v[A];
+            uint64_t n[A];
             const double lnt = ESU ? lnt_es : rl_log((double)T[0]);
 #pragma unroll
             for (int i = 0; i < A; ++i) {
-                double v = val(qi(0, s, i), ra[i]);
-                if constexpr (P == 2) v = (v + val(qi(1, s, i), rb[i])) / 2.0;
-                u[i] = ucb_value(v, p.ucb_c, lnt, (double)N[qi(0, s, i)]);
+                v[i] = val(qi(0, s, i), ra[i]);
+                if constexpr (P == 2) v[i] = (v[i] + val(qi(1, s, i), rb[i])) / 2.0;
+                n[i] = N[qi(0, s, i)];
             }
+            uint32_t need = ucb_known<A>(v, n, p.ucb_c, lnt, u);
+            // argmax (utils.rs:1-11) is decided without the unknown (finite) values
+            // when u[0] is NaN (it sticks) or some known u is +inf (the first wins)
+            bool decided = (need & 1u) == 0u && u[0] != u[0];
+#pragma unroll
+            for (int i = 0; i < A; ++i) decided = decided || (((need >> i) & 1u) == 0u && u[i] == __builtin_inf());
+            if (need && !decided) ucb_fill<A>(v, n, p.ucb_c, lnt, need, u);
             return argmax<A>(u);
         }
     };
@@ -622,17 +630,19 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
         return first;
     };
-    // owner: Q[idx] += mean of the step's contributions (clamped), clear accumulators
-    auto settle = [&](uint32_t idx) {
+    // owner: Q[idx] += mean of the step's contributions (clamped), clear
+    // accumulators; returns whether the clamp engaged (counted by the caller with
+    // a wave ballot after reconvergence: no branch, no VGPR)
+    auto settle = [&](uint32_t idx) -> bool {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
         bool hit;
         Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
-        if (hit) atomicAdd(&ACC[ACC_CLAMP], 1ull);
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
         if constexpr (SPEC) fold_flags(QF8, idx);
+        return hit;
     };
     // traces: every action of a visited state receives a contribution
     // (elegibility_traces_agent.rs:82-96), so the A entries of an LDS row share
@@ -644,23 +654,25 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     auto qi_row = [&](uint32_t tbl, uint32_t row, uint32_t a) -> uint32_t {
         return LDS_AM ? tbl * SAL + a * SL + row : tbl * SAL + row * (uint32_t)A + a;
     };
-    auto settle_row = [&](uint32_t rid) {          // rid = tbl*SL + LDS row
+    auto settle_row = [&](uint32_t rid) -> uint32_t {   // rid = tbl*SL + LDS row; returns clamp hits
         const uint32_t n = CNTR[rid];
         const double rc = n < lay.nrcp ? RCP[n] : 1.0 / (double)n;
         const uint32_t tbl = rid / SL, row = rid - tbl * SL;
+        uint32_t hits = 0;
 #pragma unroll
         for (int b = 0; b < A; ++b) {
             const uint32_t idx = qi_row(tbl, row, (uint32_t)b);
             bool hit;
             Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc), hit);
-            if (hit) atomicAdd(&ACC[ACC_CLAMP], 1ull);
+            hits += hit ? 1u : 0u;
             SUM[idx] = 0ull;
             if constexpr (SPEC) fold_flags(QF8, idx);
         }
         CNTR[rid] = 0u;
+        return hits;
     };
     // wave-level per-launch counters (scalar registers: ballot popcounts)
-    uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
+    uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0, c_clamp = 0, c_sat = 0;
     unsigned long long *const RSUM = &ACC[4];
 
     for (uint32_t k = 0; k < p.K; ++k) {
@@ -733,14 +745,26 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
                     const double lnt = lnt_es;
-                    double sum = 0.0;
+                    uint64_t n[A];
 #pragma unroll
-                    for (int i = 0; i < A; ++i) {
-                        pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)N[qi(0, s2, i)]);
-                        sum += pr[i];
+                    for (int i = 0; i < A; ++i) n[i] = N[qi(0, s2, i)];
+                    uint32_t need = ucb_known<A>(q2, n, p.ucb_c, lnt, pr);
+                    // a known non-finite u makes the sum non-finite, so some p_i is
+                    // inf/inf or NaN and the expectation is NaN: skip the rest
+                    bool nan_fq = false;
+#pragma unroll
+                    for (int i = 0; i < A; ++i) nan_fq = nan_fq || (((need >> i) & 1u) == 0u && !__builtin_isfinite(pr[i]));
+                    if (!nan_fq) {
+                        if (need) ucb_fill<A>(q2, n, p.ucb_c, lnt, need, pr);
+                        double sum = 0.0;
+#pragma unroll
+                        for (int i = 0; i < A; ++i) sum += pr[i];
+#pragma unroll
+                        for (int i = 0; i < A; ++i) pr[i] /= sum;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < A; ++i) pr[i] = __builtin_nan("");
                     }
-#pragma unroll
-                    for (int i = 0; i < A; ++i) pr[i] /= sum;
                 }
                 fq = future_q<ALGO, A>(q2, a2, pr);
             }
@@ -750,27 +774,28 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         }
         if constexpr (!TRACES) {
             const uint32_t idx = qi(ut, L.s, L.a);
-            bool owner = false;
+            bool owner = false, sat = false;
             if (train) {
                 uint32_t fl = 0;
                 int64_t dq;
-                bool sat;
                 if constexpr (SPEC) dq = q_fix(p.lr * td, fl, sat);
                 else dq = q_fix_finite(p.lr * td, sat);
-                if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
 #if RLAMD_EXP & 2   // timing experiment: no LDS atomics (results differ)
                 owner = dq == 12345;
 #else
                 owner = contribute(idx, dq, 1u, fl);
 #endif
             }
+            c_sat += (uint32_t)__popcll(__ballot(sat));
             __syncthreads();   // all contributions in, all Q reads done
+            bool hit = false;
 #if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
-            if (sweep) { if (tid < PSA && CNT16[tid] == 77) settle(tid); }
+            if (sweep) { if (tid < PSA && CNT16[tid] == 77) hit = settle(tid); }
 #else
-            if (sweep) { if (tid < PSAL) settle(tid); }
+            if (sweep) { if (tid < PSAL) hit = settle(tid); }
 #endif
-            else if (owner) settle(idx);
+            else if (owner) hit = settle(idx);
+            c_clamp += (uint32_t)__popcll(__ballot(hit));
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
@@ -870,10 +895,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
             if (rsweep) {
-                if (tid < (uint32_t)P * SL) settle_row(tid);
+                const uint32_t h = tid < (uint32_t)P * SL ? settle_row(tid) : 0u;
+                if (h) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)h);
             } else {
                 const uint32_t n_touched = LISTN[0];
-                for (uint32_t i = tid; i < n_touched; i += nthr) settle_row(LIST[i]);
+                uint32_t h = 0;
+                for (uint32_t i = tid; i < n_touched; i += nthr) h += settle_row(LIST[i]);
+                if (h) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)h);
                 __syncthreads();
                 if (tid == 0) LISTN[0] = 0u;
             }
@@ -917,6 +945,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (c_eval) atomicAdd(&ACC[1], (unsigned long long)c_eval);
             if (c_tep) atomicAdd(&ACC[2], (unsigned long long)c_tep);
             if (c_eep) atomicAdd(&ACC[3], (unsigned long long)c_eep);
+            if (c_clamp) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)c_clamp);
+            if (c_sat) atomicAdd(&ACC[ACC_SAT], (unsigned long long)c_sat);
             if (c_done) atomicAdd(&ACC[5], (unsigned long long)c_done);
         }
         if constexpr (TRACES) {

@@ -18,10 +18,10 @@ pytestmark = pytest.mark.gpu
 NEAR = (1 << 32) - 40
 
 
-def _seed_ucb(dev, ref, S, A, L=None):
+def _seed_ucb(dev, ref, S, A, L=None, spread=32):
     rng = np.random.default_rng(7)
     shape = (S, A) if L is None else (L, S, A)
-    n = (NEAR + rng.integers(0, 32, shape)).astype(np.uint64)
+    n = (NEAR + rng.integers(0, spread, shape)).astype(np.uint64)
     t = np.uint64(1 << 40) if L is None else np.full(L, 1 << 40, np.uint64)
     dev.set_ucb(n, t)
     ref.set_ucb(n, t)
@@ -53,13 +53,17 @@ def test_private_ucb_counters_cross_2p32(rl, oracle):
     p = rl.default_params(env="taxi", selector="ucb", algo="expected_sarsa", n_lanes=40, group_size=1,
                           sync_every=32)
     dev, ref = rl.Agent(p), oracle.Batch(p)
-    _seed_ucb(dev, ref, dev.S, dev.A, L=40)
+    # one agent per lane touches few of its 3000 entries: seed them at 2^32 - 2 ..
+    # 2^32 + 1 so the lanes' increments cross the u32 boundary
+    n0 = _seed_ucb(dev, ref, dev.S, dev.A, L=40, spread=4) + np.uint64(38)
+    dev.set_ucb(n0, np.full(40, 1 << 40, np.uint64))
+    ref.set_ucb(n0, np.full(40, 1 << 40, np.uint64))
     dev.run(3)
     ref.run(3)
     dn, dt = dev.ucb()
     rn, rt = ref.ucb()
     assert np.array_equal(dn, rn) and np.array_equal(dt, rt)
-    assert (dn > (1 << 32)).any()
+    assert ((n0 < (1 << 32)) & (dn >= (1 << 32))).any()
     _assert_q_equal(dev.q(), ref.q())
 
 
