@@ -12,6 +12,14 @@ the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
   python bench.py [--gpus N --steps K --warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Multi-GPU: one process per GPU, lanes partitioned by global id; the merge delta
+is all-reduced by librlamd itself (rl_comm_* / rl_agent_set_comm: RCCL int64 sum
+over xGMI, the path's only collective).  torch.distributed (gloo) is the control
+plane only: it hands rank 0's RCCL id to the other ranks, runs the barriers
+around the timed region and takes the max time over ranks.
+RLAMD_COLLECTIVE=torch swaps in a torch all_reduce of the delta (a rehearsal
+mode for ranks sharing one GPU, where RCCL cannot run).
+
 Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel
 (k_train_shared) against HBM with SURVEY §8(d)'s 32 B/env-step; `cpu_baseline`
 times the oracle's faithful single-env restatement of the reference loop on
@@ -121,16 +129,14 @@ def main():
     import torch  # loaded before librlamd so both share one HIP runtime
     import torch.distributed as dist
 
-    # one process per GPU; RLAMD_DIST_BACKEND=gloo (with ranks sharing a device)
-    # rehearses the N>1 path on a one-GPU box — the driver's runs use RCCL
-    backend = os.environ.get("RLAMD_DIST_BACKEND", "nccl")
-    dev = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
+    # one process per GPU.  collective "rccl" (default): librlamd's own RCCL
+    # all-reduce, torch's gloo group only bootstraps / times.  "torch": a
+    # dist.all_reduce of the delta (rehearsal; ranks may share a device)
+    collective = os.environ.get("RLAMD_COLLECTIVE", "rccl")
+    dev = local_rank if collective == "rccl" else local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group(os.environ.get("RLAMD_DIST_BACKEND", "gloo"))
     import rlamd
 
     p = rlamd.default_params(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
@@ -143,17 +149,22 @@ def main():
     stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
     torch.cuda.set_stream(stream)
     agent.set_stream(stream.cuda_stream)
-    delta = None
-    if world > 1:
+    delta, comm = None, None
+    if world > 1 and collective == "rccl":
+        box = [rlamd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = rlamd.Comm(rank, world, box[0], dev)
+        agent.set_comm(comm)                # every merge: RCCL int64 sum of the delta, then apply
+    elif world > 1:
         delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
 
     def step():
-        if delta is None:                   # one process: launch + merge (fused fold/apply where possible)
+        if delta is None:                   # launch + merge (librlamd: RCCL all-reduce when world > 1)
             agent.run(1)
             return
-        agent.launch_train()
-        dist.all_reduce(delta)              # ΔQ / ΔN / Δt: exact int64 sum over ranks (RCCL)
+        agent.launch_train()                # rehearsal: torch all_reduce of the delta
+        dist.all_reduce(delta)
         agent.launch_apply()
 
     for _ in range(args.warmup):
@@ -181,12 +192,11 @@ def main():
     # RESET steps (env.reset + first get_action) are not env steps
     steps_done = st1["train_steps"] - st0["train_steps"]
     assert 0 < steps_done <= args.steps * args.sync * args.lanes, steps_done
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{dev}")
+    if world > 1:                           # control plane (gloo, host tensors)
+        t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-    if world > 1:
-        ts = torch.tensor([steps_done], dtype=torch.int64, device=f"cuda:{dev}")
+        ts = torch.tensor([steps_done], dtype=torch.int64)
         dist.all_reduce(ts)
         total_steps = int(ts.item())
     else:
@@ -220,6 +230,8 @@ def main():
                    "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
+                   "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"
+                                  else "torch all_reduce (rehearsal)") if world > 1 else "none",
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"]},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
@@ -235,6 +247,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     agent.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

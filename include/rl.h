@@ -38,7 +38,8 @@ enum rl_status {
     RL_E_ARG = 2,       /* invalid argument / size */
     RL_E_HIP = 3,       /* HIP runtime failure */
     RL_E_OOM = 4,       /* device allocation failed */
-    RL_E_STATE = 5      /* call not valid in the handle's current mode */
+    RL_E_STATE = 5,     /* call not valid in the handle's current mode */
+    RL_E_RCCL = 6       /* RCCL (collective) failure */
 };
 
 enum rl_env_kind {      /* src/env/{frozen_lake,cliff_walking,taxi,blackjack,frozen_lake_edited}.rs */
@@ -165,6 +166,7 @@ typedef struct rl_stats {
 
 typedef struct rl_env rl_env;
 typedef struct rl_agent rl_agent;
+typedef struct rl_comm rl_comm;
 
 /* ---------------------------------------------------------------- misc */
 const char *rl_last_error(void);
@@ -267,6 +269,26 @@ int rl_agent_get_weights(rl_agent *a, double *out, size_t n);
 int rl_agent_set_weights(rl_agent *a, const double *in, size_t n);
 /* the input-adapter features of every dense state, [n_states][n_in] (no GPU needed) */
 int rl_net_features(const rl_env_config *env, int32_t input, double *out, size_t n);
+
+/* -------- multi-GPU (SURVEY 8(b) rl_sync, 8(e)): one process per GPU, lanes
+ * partitioned contiguously (lane_offset = rank * n_lanes).  The ONLY collective is
+ * an RCCL int64 sum of the merge delta (ΔQ, group counts, ΔN, Δt, flag counts)
+ * over xGMI after every launch; integer sums make Q identical for any rank count.
+ * Bootstrap: rank 0 calls rl_comm_unique_id and hands the bytes to every rank
+ * (any channel: MPI, a file, the launcher), then each rank calls rl_comm_init. */
+#define RL_COMM_ID_BYTES 128
+int rl_comm_unique_id(void *id_out /* RL_COMM_ID_BYTES */);
+int rl_comm_init(int32_t rank, int32_t world, const void *id /* RL_COMM_ID_BYTES */, int32_t device,
+                 rl_comm **out);
+void rl_comm_destroy(rl_comm *c);
+int rl_comm_rank(rl_comm *c, int32_t *rank, int32_t *world);
+/* attach (NULL: detach) a communicator: from then on every merge of rl_agent_run /
+ * rl_agent_train / rl_agent_evaluate all-reduces the delta over it (train/evaluate
+ * also agree on termination across ranks).  Shared mode only. */
+int rl_agent_set_comm(rl_agent *a, rl_comm *c);
+/* the merge of one rl_agent_launch_train: all-reduce the delta over the attached
+ * communicator (none: this rank alone) on the agent's stream, then Q_base += Δ */
+int rl_agent_sync(rl_agent *a);
 
 /* -------- multi-GPU: the ΔQ merge as an external collective (shared mode) */
 /* number of int64 words of the merge delta (ΔQ, ΔN, Δt, Δflags) */

@@ -4,6 +4,7 @@
 // only allocates, copies and launches.  There is no CPU fallback: without a
 // HIP device every compute entry point returns RL_E_HIP.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -319,7 +320,20 @@ void dfree(T *&p) {
 
 }  // namespace
 
+#define NCCLC(expr)                                                                                \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess) return fail(RL_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
 // ====================================================================== handles
+// One RCCL communicator per process (one GPU per rank): the only
+// collective of the path is the int64 sum of the merge delta over xGMI.
+struct rl_comm {
+    ncclComm_t comm = nullptr;
+    int32_t rank = 0, world = 1, device = 0;
+    int64_t *word = nullptr;   // one device int64 for the done-lane agreement of train()/evaluate()
+};
 struct rl_env {
     rl_env_config cfg{};
     EnvHost eh;
@@ -391,6 +405,7 @@ struct rl_agent {
     train_launch_fn fn = nullptr;
     dim3 grid, block;
     size_t smem = 0;
+    rl_comm *comm = nullptr;   // multi-GPU: the merge delta is all-reduced over it
 };
 
 namespace {
@@ -581,7 +596,7 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
     }
     if (merge) *merge = false;
     if (!a->priv) {                       // fold the group-delta replicas into the delta
-        if (merge && a->delta == a->delta_own && a->cfg.selector != RL_SEL_UCB) {
+        if (merge && a->delta == a->delta_own && a->cfg.selector != RL_SEL_UCB && !a->comm) {
             launch_fold_apply(a->kp, a->stream);   // ... and apply it (eps-greedy: sums + counts only)
             *merge = true;
         } else {
@@ -610,6 +625,36 @@ int launch_apply_kernel(rl_agent *a) {
     return RL_OK;
 }
 
+// the merge's collective: this rank's delta (already folded from the group
+// replicas) summed over every rank, in place, on the agent's stream.  Exact
+// int64 sums, so Q is bit-identical for any rank count at a fixed global lane set.
+int allreduce_delta(rl_agent *a) {
+    if (!a->comm) return RL_OK;   // no communicator: this process's delta is the total
+    NCCLC(ncclAllReduce(a->delta, a->delta, a->delta_words, ncclInt64, ncclSum, a->comm->comm, a->stream));
+    return RL_OK;
+}
+// one launch of K steps + the merge (fused fold+apply for a one-process eps-greedy learner)
+int launch_and_merge(rl_agent *a) {
+    bool merged = false;
+    int rc = launch_train_kernel(a, &merged);
+    if (rc) return rc;
+    if (merged) return RL_OK;
+    if ((rc = allreduce_delta(a))) return rc;
+    return launch_apply_kernel(a);
+}
+// sum of a host value over the ranks (1 rank: itself)
+int allreduce_u64(rl_agent *a, uint64_t v, uint64_t *sum) {
+    *sum = v;
+    if (!a->comm) return RL_OK;
+    int64_t x = (int64_t)v;
+    HIPC(hipMemcpyAsync(a->comm->word, &x, 8, hipMemcpyHostToDevice, a->stream));
+    NCCLC(ncclAllReduce(a->comm->word, a->comm->word, 1, ncclInt64, ncclSum, a->comm->comm, a->stream));
+    HIPC(hipMemcpyAsync(&x, a->comm->word, 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    *sum = (uint64_t)x;
+    return RL_OK;
+}
+
 int run_until_done(rl_agent *a, rl_stats *out) {
     // stats slot 5 counts lanes that are DONE at the end of a launch.  Guards: a
     // lane needs at most (max_steps + 1) steps per episode, so a call that has
@@ -621,10 +666,8 @@ int run_until_done(rl_agent *a, rl_stats *out) {
             return fail(RL_E_OOM, "recorded stream exceeds 4 GiB: record fewer steps");
         // done-lane counter (slot 5 of every stats replica) is per launch
         HIPC(hipMemset2DAsync(&a->stats_d[5], STATS_W * 8, 0, 8, STATS_REP, a->stream));
-        bool merged = false;
-        int rc = launch_train_kernel(a, &merged);
+        int rc = launch_and_merge(a);
         if (rc) return rc;
-        if (!merged && (rc = launch_apply_kernel(a))) return rc;
         std::vector<unsigned long long> st(STATS_W * STATS_REP);
         HIPC(hipMemcpyAsync(st.data(), a->stats_d, st.size() * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
@@ -635,7 +678,11 @@ int run_until_done(rl_agent *a, rl_stats *out) {
             HIPC(hipMemcpy(c.data(), a->core, a->L * 16, hipMemcpyDeviceToHost));
             if (FILE *f = fopen(dump, "ab")) { fwrite(c.data(), 16, a->L, f); fclose(f); }
         }
-        if (done >= a->L) break;
+        // every rank runs the same number of launches (each one all-reduces):
+        // stop when the lanes of ALL ranks are done
+        uint64_t done_all = 0, lanes_all = 0;
+        if ((rc = allreduce_u64(a, done, &done_all)) || (rc = allreduce_u64(a, a->L, &lanes_all))) return rc;
+        if (done_all >= lanes_all) break;
     }
     if (out) return rl_agent_stats(a, out);
     return RL_OK;
@@ -1044,10 +1091,8 @@ int rl_agent_run(rl_agent *a, uint32_t n) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
     for (uint32_t i = 0; i < n; ++i) {
-        bool merged = false;
-        int rc = launch_train_kernel(a, &merged);
+        const int rc = launch_and_merge(a);
         if (rc) return rc;
-        if (!merged && (rc = launch_apply_kernel(a))) return rc;
     }
     return RL_OK;
 }
@@ -1340,6 +1385,66 @@ int rl_agent_launch_train(rl_agent *a) {
 int rl_agent_launch_apply(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
+    return launch_apply_kernel(a);
+}
+
+int rl_comm_unique_id(void *id_out) {
+    if (!id_out) return fail(RL_E_ARG, "null argument");
+    static_assert(sizeof(ncclUniqueId) == RL_COMM_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId id;
+    NCCLC(ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof id);
+    return RL_OK;
+}
+
+int rl_comm_init(int32_t rank, int32_t world, const void *id_in, int32_t device, rl_comm **out) {
+    if (!id_in || !out || world < 1 || rank < 0 || rank >= world) return fail(RL_E_ARG, "bad rank / world / id");
+    *out = nullptr;
+    HIPC(hipSetDevice(device));
+    rl_comm *c = new rl_comm();
+    c->rank = rank; c->world = world; c->device = device;
+    ncclUniqueId id;
+    memcpy(&id, id_in, sizeof id);
+    const ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) { delete c; return fail(RL_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); }
+    if (hipMalloc((void **)&c->word, 8) != hipSuccess) {
+        (void)ncclCommDestroy(c->comm);
+        delete c;
+        return fail(RL_E_OOM, "comm word");
+    }
+    *out = c;
+    return RL_OK;
+}
+
+void rl_comm_destroy(rl_comm *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->word) (void)hipFree(c->word);
+    delete c;
+}
+
+int rl_comm_rank(rl_comm *c, int32_t *rank, int32_t *world) {
+    if (!c || !rank || !world) return fail(RL_E_ARG, "null argument");
+    *rank = c->rank;
+    *world = c->world;
+    return RL_OK;
+}
+
+int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (c && a->priv) return fail(RL_E_STATE, "private mode (group_size 1) has no merge to reduce");
+    if (c && c->device != a->device) return fail(RL_E_ARG, "communicator and agent on different devices");
+    a->comm = c;
+    return RL_OK;
+}
+
+int rl_agent_sync(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    if (a->priv) return RL_OK;
+    HIPC(hipSetDevice(a->device));
+    int rc = allreduce_delta(a);
+    if (rc) return rc;
     return launch_apply_kernel(a);
 }
 

@@ -130,7 +130,14 @@ SIGNATURES = {
     "rl_agent_get_weights": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_set_weights": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_net_features": (C.c_int, [_P(EnvConfig), C.c_int32, _V, C.c_size_t]),
+    "rl_comm_unique_id": (C.c_int, [_V]),
+    "rl_comm_init": (C.c_int, [C.c_int32, C.c_int32, _V, C.c_int32, _P(_V)]),
+    "rl_comm_destroy": (None, [_V]),
+    "rl_comm_rank": (C.c_int, [_V, _P(C.c_int32), _P(C.c_int32)]),
+    "rl_agent_set_comm": (C.c_int, [_V, _V]),
+    "rl_agent_sync": (C.c_int, [_V]),
 }
+COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -417,6 +424,15 @@ class Agent:
     def launch_apply(self):
         check(lib().rl_agent_launch_apply(self.h))
 
+    def set_comm(self, comm):
+        """all-reduce every merge over an RCCL communicator (None: detach)"""
+        self._comm = comm                     # keep it alive while attached
+        check(lib().rl_agent_set_comm(self.h, comm.h if comm is not None else None))
+
+    def sync(self):
+        """the merge after launch_train(): RCCL all-reduce of the delta, then apply"""
+        check(lib().rl_agent_sync(self.h))
+
     def set_stream(self, stream_ptr):
         check(lib().rl_agent_set_stream(self.h, C.c_void_p(stream_ptr)))
 
@@ -432,6 +448,33 @@ class Agent:
         ms, n = C.c_double(), C.c_uint64()
         check(lib().rl_agent_get_timing(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+
+def comm_unique_id():
+    """RCCL unique id (bytes) made on rank 0; hand it to every rank"""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    check(lib().rl_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """rl_comm: one RCCL communicator per process (one GPU per rank)"""
+
+    def __init__(self, rank, world, uid, device=0):
+        assert len(uid) == COMM_ID_BYTES
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().rl_comm_init(rank, world, buf, device, C.byref(h)))
+        self.h = h
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rl_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def kat_log(x, device=0):

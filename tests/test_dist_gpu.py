@@ -1,6 +1,6 @@
 """N>1 rehearsal on the one-GPU box (gloo, 2 ranks sharing the device).
 
-The driver runs bench.py at N = 2/4/8 over RCCL on a whole node; these tests
+The driver runs bench.py at N = 2/4/8 over RCCL (librlamd's rl_comm) on a whole node; these tests
 exercise the same per-rank code path on real hardware:
   - the per-rank merge (launch_train -> all_reduce(int64 delta) -> launch_apply)
     gives raw Q / UCB counters bit-identical to one process holding every lane;
@@ -28,7 +28,9 @@ def _free_port():
 
 
 def _torchrun(args, n=2, timeout=240):
-    env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    # two ranks share the one GPU, so the merge goes through torch's all_reduce
+    # (bench.py RLAMD_COLLECTIVE=torch); RCCL itself is exercised by test_gpu_rccl.py
+    env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", RLAMD_COLLECTIVE="torch", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
