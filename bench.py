@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--slippery", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--counters-file", default=os.path.join(ROOT, "profiles", "counters.json"),
+                    help="PMC summaries per workload (scripts/collect_counters.py)")
     a = ap.parse_args()
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
@@ -75,6 +76,24 @@ PRESETS = {
     5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
             lanes=1 << 19, group=512),
 }
+
+
+def workload_key(args):
+    return f"cfg{args.config}" + ("_slippery" if args.slippery else "")
+
+
+def counters_for(args):
+    """PMC summary of the dominant kernel for this exact workload, or None"""
+    try:
+        tab = json.load(open(args.counters_file))
+    except (OSError, ValueError):
+        return None
+    c = tab.get(workload_key(args))
+    if not c:
+        return None
+    want = {"env": args.env, "algo": args.algo, "lanes": args.lanes, "group": args.group, "sync": args.sync,
+            "slippery": args.slippery}
+    return c if all(c.get(k) == v for k, v in want.items()) else None
 
 
 def cpu_baseline(args):
@@ -210,21 +229,16 @@ def main():
     bytes_per_step = BYTES_PER_STEP + (16 * n_act + 2) * v_bar
     bytes_per_launch = bytes_per_step * steps_done / args.steps
     achieved = bytes_per_launch / avg_kern_s
-    traffic = None
-    if os.path.exists(args.traffic_file):
-        try:
-            tf = json.load(open(args.traffic_file))
-            if (tf.get("lanes") == args.lanes and tf.get("sync") == args.sync and tf.get("env") == args.env
-                    and tf.get("group") == args.group and tf.get("algo") == args.algo):
-                traffic = tf.get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+    pmc = counters_for(args)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    issue = pmc.get("valu_busy_frac") if pmc else None
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (env lanes seeded per global lane id; no dataset)",
-        "config": {"workload": f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
+        "config": {"workload": f"run mode (rl_agent_run: lanes train continuously, eval interleave off) "
+                               f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
                    "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
@@ -233,14 +247,28 @@ def main():
                    "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"
                                   else "torch all_reduce (rehearsal)") if world > 1 else "none",
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"]},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+        # `frac` prices SURVEY §8(d)'s algorithmic bytes (32 B/env-step) against HBM
+        # peak; the fused kernel keeps lane records in registers for K steps, so the
+        # PMC-measured traffic is far below them and the binding limit is on-chip
+        # issue / LDS: `traffic_frac` (measured bytes) and `issue_frac` (VALU busy)
+        # say how close each is to its own ceiling.
+        "roofline": {"bound": "hbm", "basis": "priced algorithmic bytes (SURVEY 8(d)), not measured traffic",
+                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
+                     "traffic_frac": (traffic / avg_kern_s / HBM_PEAK) if traffic else None,
+                     "issue_frac": issue,
+                     "counters": pmc.get("source") if pmc else None,
                      "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
                      "kernel_launches": n_kern,
                      "bytes_per_launch": bytes_per_launch, "bytes_per_env_step": bytes_per_step,
                      **({"trace_v_bar": v_bar} if args.agent == "traces" else {})},
         "torch_event_ms": ev0.elapsed_time(ev1),
+        # shared-mode fixed-point health over the timed window: Q entries the
+        # |Q| <= 2048 clamp held, TD deltas saturated at +-2^51 raw (0 = the run
+        # is the reference's f64 arithmetic)
+        "q_clamp_hits": st1["q_clamp_hits"] - st0["q_clamp_hits"],
+        "delta_saturations": st1["delta_saturations"] - st0["delta_saturations"],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -406,6 +407,7 @@ struct rl_agent {
     dim3 grid, block;
     size_t smem = 0;
     rl_comm *comm = nullptr;   // multi-GPU: the merge delta is all-reduced over it
+    double q_abs0 = 0.0;       // shared mode: max |Q| the table was last reset / set to (hits_proven_zero)
 };
 
 namespace {
@@ -497,6 +499,7 @@ int agent_reset_policy(rl_agent *a) {
     } else {
         uint32_t fl = 0;
         const int64_t d = q_fix(a->cfg.q_default, fl);
+        a->q_abs0 = std::fabs(a->cfg.q_default);
         std::vector<int64_t> q(PSA, d);
         std::vector<uint32_t> f(PSA, fl);
         HIPC(hipMemcpyAsync(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice, a->stream));
@@ -554,6 +557,53 @@ int agent_reset_selector(rl_agent *a) {
     return RL_OK;
 }
 
+// max |reward| an env step can return, truncation included
+double env_reward_bound(int kind) {
+    switch (kind) {
+    case RL_ENV_FROZEN_LAKE: return 1.0;           // frozen_lake.rs:44 (0/1), :121 (0)
+    case RL_ENV_FROZEN_LAKE_EDITED: return 10.0;   // frozen_lake_edited.rs (+10 goal, -1 otherwise)
+    case RL_ENV_CLIFF_WALKING: return 100.0;       // cliff_walking.rs (-100 cliff / truncation, -1)
+    case RL_ENV_TAXI: return 20.0;                 // taxi.rs:76-110 (+20, -10, -1), truncation 0
+    case RL_ENV_BLACKJACK: return 1.0;             // blackjack.rs (+-1, 0)
+    default: return std::numeric_limits<double>::infinity();
+    }
+}
+
+// Can a shared-mode entry reach the |Q| <= 2048 clamp, or a TD delta saturate at
+// +-2^51 raw?  Not when the bootstrap F is a sub-convex combination of Q values —
+// SARSA's pick, Q-learning's max, expected SARSA over eps-greedy's probabilities
+// (eps/A each and 1-eps at the argmax: non-negative for eps in [0,1], summing to
+// 1-eps/A; src/agent.rs:19-45, uniform_epsilon_greed.rs:72-76).  Then one update
+// Q' = (1-w)Q + w(r + gamma*F), w = lr*E in [0,1] (E = the trace, <= 1/(1-gamma*
+// lambda) for the accumulating trace, 1 for one-step), keeps |Q'| <= max(M,
+// R/(1-gamma)) when |Q|, |F| <= M; a step's mean of such values and the merge's
+// mean over groups keep the bound, so by induction every entry stays within
+// Mb = max(|Q_0|, R/(1-gamma)), and every delta within lr*E*(R + (1+gamma)Mb).
+// UCB + expected SARSA weighs by u_i / sum(u) (upper_confidence_bound.rs:48-63):
+// no bound, its kernels always count.
+bool hits_proven_zero(const rl_agent *a) {
+    const rl_agent_config &c = a->cfg;
+    if (a->priv || a->neural) return false;
+    if (c.selector == RL_SEL_UCB && c.algo == RL_ALGO_EXPECTED_SARSA) return false;
+    const double lr = c.lr, g = c.gamma;
+    if (!(lr >= 0.0 && g >= 0.0 && g < 1.0 && std::isfinite(a->q_abs0))) return false;
+    double emax = 1.0;
+    if (c.agent == RL_AGENT_TRACES) {
+        const double gl = g * c.lambda;
+        if (!(gl >= 0.0 && gl < 1.0)) return false;
+        emax = 1.0 / (1.0 - gl);
+    }
+    if (!(lr * emax <= 1.0)) return false;
+    if (c.selector == RL_SEL_EPS_GREEDY && c.algo == RL_ALGO_EXPECTED_SARSA) {
+        // eps stays in [eps_final, eps0] (or decays toward 0 by a factor in [0,1])
+        const bool dec = c.decay_kind == RL_DECAY_MUL ? (c.eps_decay >= 0.0 && c.eps_decay <= 1.0) : c.eps_decay >= 0.0;
+        if (!(c.eps0 >= 0.0 && c.eps0 <= 1.0 && c.eps_final >= 0.0 && dec)) return false;
+    }
+    const double R = env_reward_bound(c.env.kind);
+    const double mb = std::max(a->q_abs0, R / (1.0 - g));
+    return mb <= 2000.0 && lr * emax * (R + (1.0 + g) * mb) < 2000.0;
+}
+
 void agent_sync_params(rl_agent *a) {
     KParams &p = a->kp;
     p.lr = a->cfg.lr;
@@ -564,6 +614,7 @@ void agent_sync_params(rl_agent *a) {
     p.ucb_c = a->cfg.ucb_c;
     p.decay_kind = a->cfg.decay_kind;
     p.algo = a->cfg.algo;
+    p.hits_zero = hits_proven_zero(a) ? 1 : 0;
     p.delta = a->delta;
     p.plan_steps = a->plan;
     p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;
@@ -1194,7 +1245,11 @@ int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
     if (n < PSA) return fail(RL_E_ARG, "input too small");
     std::vector<int64_t> q(PSA);
     std::vector<uint32_t> f(PSA, 0);
-    for (size_t i = 0; i < PSA; ++i) q[i] = q_fix(in[i], f[i]);
+    a->q_abs0 = 0.0;
+    for (size_t i = 0; i < PSA; ++i) {
+        q[i] = q_fix(in[i], f[i]);
+        a->q_abs0 = std::isnan(in[i]) ? std::numeric_limits<double>::infinity() : std::max(a->q_abs0, std::fabs(in[i]));
+    }
     HIPC(hipMemcpy(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice));
     bj_term_scan(a, q.data(), f.data());
@@ -1457,6 +1512,7 @@ int rl_agent_set_stream(rl_agent *a, void *stream) {
 int rl_agent_occupancy(rl_agent *a, uint32_t *groups_per_cu, uint64_t *lds_bytes, uint32_t *block_threads) {
     if (!a || !groups_per_cu || !lds_bytes || !block_threads) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
+    agent_sync_params(a);   // the kernel choice depends on KParams::hits_zero
     int n = 0;
     HIPC(a->fn(a->kp, a->grid, a->block, a->smem, a->stream, &n));
     *groups_per_cu = (uint32_t)n;

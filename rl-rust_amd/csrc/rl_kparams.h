@@ -91,6 +91,11 @@ struct KParams {
     // hyper-parameters
     double lr, gamma, gl, eps_decay, eps_final, ucb_c;
     int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
+    // the host proved that no shared-mode Q entry can reach the +-2048 clamp and no
+    // TD delta can saturate for these hyper-parameters (rl_host.cpp hits_proven_zero):
+    // the throughput kernels then skip counting rl_stats::q_clamp_hits /
+    // delta_saturations (both provably 0)
+    int32_t hits_zero;
     // train()/evaluate() control
     uint64_t target_episodes, eval_at;
     uint64_t eval_div;     // ceil(2^64 / eval_at) (mod 2^64): divisibility test constant

@@ -464,7 +464,10 @@ __device__ __forceinline__ void fold_flags(uint8_t *QF8, uint32_t idx) {
 // ======================================================================== shared
 // INSTR: step records / episode log compiled in (chosen at launch when either is
 // enabled); the throughput variant carries neither.
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1>
+// HITS: count clamp hits / delta saturations (off only where the host proved both 0:
+// KParams::hits_zero)
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1,
+          bool HITS = true>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -637,8 +640,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const uint32_t n = CNT16[idx];
         const int64_t sum = (int64_t)SUM[idx];
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
-        bool hit;
-        Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
+        bool hit = false;
+        if constexpr (HITS) Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
+        else Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
         SUM[idx] = 0ull;
         CNT16[idx] = 0;
         if constexpr (SPEC) fold_flags(QF8, idx);
@@ -786,7 +790,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 owner = contribute(idx, dq, 1u, fl);
 #endif
             }
-            c_sat += (uint32_t)__popcll(__ballot(sat));
+            if constexpr (HITS) c_sat += (uint32_t)__popcll(__ballot(sat));
             __syncthreads();   // all contributions in, all Q reads done
             bool hit = false;
 #if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
@@ -795,7 +799,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (sweep) { if (tid < PSAL) hit = settle(tid); }
 #endif
             else if (owner) hit = settle(idx);
-            c_clamp += (uint32_t)__popcll(__ballot(hit));
+            if constexpr (HITS) c_clamp += (uint32_t)__popcll(__ballot(hit));
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
@@ -998,9 +1002,14 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
 // FrozenLake / CliffWalking and one-step eps-greedy Blackjack.  The other
 // variants would spill for no occupancy.
+// It counts clamp hits / delta saturations only for UCB + expected SARSA (SURVEY
+// F7: unbounded bootstrap weights); every other configuration runs it only when
+// the host proved both counts 0 (KParams::hits_zero), else k_train_shared.
+template <int SEL, int ALGO>
+constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA; }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>()>(p);
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
@@ -1250,6 +1259,7 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
         k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, true>;
     } else {
         if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) {
+          if (o8_counts_hits<SEL, ALGO>() || p.hits_zero) {
             // the map's slippery flag as a compile-time constant (FrozenLake only)
             // the map's slippery flag (FrozenLake) and the settle form (every entry
             // owned by one thread when P*S*A <= block size) as compile-time constants
@@ -1263,6 +1273,9 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
                 k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>
                        : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>;
             }
+          } else {
+            k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+          }
         } else {
             k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         }

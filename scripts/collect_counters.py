@@ -1,0 +1,66 @@
+"""File one workload's rocprofv3 evidence (scripts/profile.sh output dir) under
+profiles/: <round>_<key>_kernel_stats.csv, <round>_<key>_summary.json, and the
+entry bench.py reads back for `roofline.traffic` / `issue_frac`
+(profiles/counters.json, keyed by workload: cfg2, cfg2_slippery, cfg3, ...).
+
+    python scripts/collect_counters.py gpurun_out/prof_r02_cfg3 r02 --config 3 [--slippery 1]
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+from summarize_profile import summarize  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("profdir")
+    ap.add_argument("round")
+    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--slippery", type=int, default=0)
+    ap.add_argument("--kernel", default="k_train_shared")
+    a = ap.parse_args()
+    import bench
+    pr = bench.PRESETS[a.config]
+    key = f"cfg{a.config}" + ("_slippery" if a.slippery else "")
+    s = summarize(a.profdir, a.kernel)
+    prof = os.path.join(ROOT, "profiles")
+    stem = f"{a.round}_{key}"
+    shutil.copy(os.path.join(a.profdir, "trace", "run_kernel_stats.csv"),
+                os.path.join(prof, stem + "_kernel_stats.csv"))
+    try:
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                              text=True).stdout.strip()
+    except OSError:
+        head = "?"
+    s["dir"] = f"{a.profdir} (copied; build at HEAD {head or '?'})"
+    json.dump(s, open(os.path.join(prof, stem + "_summary.json"), "w"), indent=1)
+    path = os.path.join(prof, "counters.json")
+    tab = json.load(open(path)) if os.path.exists(path) else {}
+    hb = s.get("hbm_bytes_per_launch", {})
+    tab[key] = {"env": pr["env"], "algo": pr["algo"], "lanes": pr["lanes"], "group": pr["group"],
+                "sync": 64, "slippery": a.slippery,
+                "hbm_bytes_per_launch": hb.get("total"),
+                "valu_busy_frac": s.get("valu_busy_frac"),
+                "lds_active_frac": s.get("lds_active_frac"),
+                "lds_bank_conflict_frac": (s["pmc_mean_per_launch"].get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                           s["pmc_mean_per_launch"]["SQ_LDS_IDX_ACTIVE"])
+                if "SQ_LDS_IDX_ACTIVE" in s["pmc_mean_per_launch"] else None,
+                "wave_cycle_split": s.get("wave_cycle_split"),
+                "kernel_avg_ns": s.get("kernel_avg_ns"),
+                "source": f"profiles/{stem}_summary.json: rocprofv3 separate --pmc passes (FETCH_SIZE x2 "
+                          f"gfx950 correction + WRITE_SIZE; SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE/8 x 1024 "
+                          f"SIMDs)), mean per launch of the dominant kernel, HEAD {head}"}
+    json.dump(tab, open(path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(tab[key], indent=1))
+
+
+if __name__ == "__main__":
+    main()
