@@ -54,7 +54,7 @@ def parse():
         ap.add_argument("--" + k, default=None)
     ap.add_argument("--map8x8", type=int, default=1)
     ap.add_argument("--slippery", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--counters-file", default=os.path.join(ROOT, "profiles", "counters.json"),
                     help="PMC summaries per workload (scripts/collect_counters.py)")
@@ -97,46 +97,74 @@ def counters_for(args):
 
 
 def cpu_baseline(args):
-    """Faithful single-env restatement of the reference loop (oracle, 1 core),
-    FrozenLake-8x8 Q-learning eps-greedy, no eval interleave; sample sized to
-    ~cpu_seconds of work."""
-    exe = os.path.join(ROOT, "oracle", "_build", "rlref_bench")
-    if not os.path.exists(exe):
+    """SURVEY §8(d) CPU reference timing, on this host's cores, bounded samples.
+
+    value  — "ref_faithful" (oracle/ref_faithful.c): the reference's single-env
+             loop with its own data structures (FxHashMap Q, per-step TD Vec push,
+             ChaCha12 draws, eval interleave every n/10 episodes), the bench's
+             workload (FrozenLake 8x8 Q-learning eps-greedy) at the CLI defaults
+             (n_episodes 1e5, src/bin/frozen_lake.rs:35-73), 1 core; whole training
+             runs repeated (train -> reset, as the bins' sweep) until the sample
+             lasts about `cpu_seconds`.
+    multi_core — the same, one independent env per thread (16: the box's share).
+    cfg1   — SURVEY cfg 1: FrozenLake 4x4 one-step Q-learning eps-greedy, 1 core.
+    ref_dense — the oracle's dense-array restatement of the same loop, 1 core.
+    Non-FrozenLake workloads report ref_dense only (ref_faithful covers FrozenLake).
+    Every number is a C restatement of the reference loop, not the Rust binary
+    (no Rust toolchain here: SURVEY §8(c))."""
+    odir = os.path.join(ROOT, "oracle", "_build")
+    rf, dense = os.path.join(odir, "ref_faithful"), os.path.join(odir, "rlref_bench")
+    if not (os.path.exists(rf) and os.path.exists(dense)):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     envk = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}[args.env]
     agentk = {"one_step": 0, "traces": 1}[args.agent]
     polk = {"tabular": 0, "double": 1}[args.policy]
     selk = {"eps_greedy": 0, "ucb": 1}[args.selector]
     algok = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}[args.algo]
+    n, eval_at = 100000, 10000          # the bins: train(env, n_episodes, n_episodes / 10)
 
-    def run(n, threads=1):
-        out = subprocess.run([exe, str(envk), str(args.map8x8), str(args.slippery), str(agentk),
-                              str(polk), str(selk), str(algok), str(n), "0", str(threads)],
+    def run_rf(map8, reps, threads):
+        out = subprocess.run([rf, str(map8), str(args.slippery), str(selk), str(algok), str(n), str(eval_at),
+                              str(reps), str(threads)], check=True, capture_output=True, text=True).stdout
+        return json.loads(out)
+
+    def run_dense(reps, threads):
+        out = subprocess.run([dense, str(envk), str(args.map8x8), str(args.slippery), str(agentk), str(polk),
+                              str(selk), str(algok), str(n), str(eval_at), str(threads), str(reps)],
                              check=True, capture_output=True, text=True).stdout
         return json.loads(out)
 
-    def sized(threads, target):
-        # episode length depends on n (the eps decay spans 0.5*n episodes), so
-        # grow n until one run takes about `target` seconds
-        n, r = 20000, run(20000, threads)
-        while r["seconds"] < 0.6 * target and n < (1 << 34):
-            n = int(n * min(8.0, max(1.5, target / max(r["seconds"], 1e-3))))
-            r = run(n, threads)
-        return n, r
+    def sized(fn, target):
+        reps, r = 1, fn(1)
+        while r["seconds"] < 0.6 * target and reps < 1 << 20:
+            reps = max(reps + 1, int(reps * min(8.0, target / max(r["seconds"], 1e-3))))
+            r = fn(reps)
+        return reps, r
 
-    n, r = sized(1, args.cpu_seconds)
-    res = {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": 1, "kind": "port",
-           "sample": f"oracle faithful single-env loop (src/agent.rs:66-118 restated in C), "
-                     f"{args.env} {'8x8' if args.map8x8 else '4x4'} {args.agent} {args.algo} "
-                     f"{args.selector}, {n} episodes = {r['steps']} env-steps in {r['seconds']:.2f} s"}
-    # SURVEY §8(d)(ii): one independent faithful env per host core (the box's CPU
-    # share is 16 threads; os.cpu_count() reports the whole machine)
-    threads = min(16, os.cpu_count() or 1)
-    if threads > 1:
-        m_n, m = sized(threads, args.cpu_seconds / 2)
-        res["multi_core"] = {"value": m["steps_per_sec"], "cores": threads,
-                             "sample": f"{threads} independent faithful envs x {m_n} episodes, "
-                                       f"{m['steps']} env-steps in {m['seconds']:.2f} s"}
+    def line(kind, what, reps, r, threads):
+        return {"value": r["steps_per_sec"], "unit": "env-steps/s", "cores": threads, "kind": "port",
+                "sample": f"{what}: {reps} x train({n} episodes, eval every {eval_at}) per core = "
+                          f"{r['steps']} training env-steps in {r['seconds']:.2f} s"}
+
+    threads = min(16, os.cpu_count() or 1)     # the box's CPU share; os.cpu_count() is the machine
+    fl = args.env == "frozen_lake" and args.agent == "one_step" and args.policy == "tabular"
+    desc = (f"{args.env}{' 8x8' if args.map8x8 else ''}{' slippery' if args.slippery else ''} "
+            f"{args.agent} {args.algo} {args.selector}")
+    if fl:
+        reps, r = sized(lambda k: run_rf(args.map8x8, k, 1), args.cpu_seconds)
+        res = line("port", f"ref_faithful (oracle/ref_faithful.c: FxHashMap Q, ChaCha12, Vec histories) {desc}",
+                   reps, r, 1)
+        reps_m, m = sized(lambda k: run_rf(args.map8x8, k, threads), args.cpu_seconds / 2)
+        res["multi_core"] = line("port", f"{threads} independent ref_faithful envs", reps_m, m, threads)
+        reps1, c1 = sized(lambda k: run_rf(0, k, 1), args.cpu_seconds / 4)
+        res["cfg1"] = line("port", "SURVEY cfg 1: ref_faithful FrozenLake 4x4 one-step Q-learning eps-greedy",
+                           reps1, c1, 1)
+    repd, d = sized(lambda k: run_dense(k, 1), args.cpu_seconds / (4 if fl else 1))
+    dl = line("port", f"ref_dense (oracle/rlref.c rlo_faithful: dense-array Q) {desc}", repd, d, 1)
+    if not fl:
+        return dl
+    res["ref_dense"] = dl
+    res["host_threads_available"] = os.cpu_count()
     return res
 
 

@@ -1,13 +1,17 @@
 /*
- * rlref_bench.c — CPU baseline timer (test/bench infrastructure only).
+ * rlref_bench.c — CPU baseline timer (test/bench infrastructure only): "ref_dense".
  *
- * Times the faithful single-env restatement of the reference training loop
- * (src/agent.rs:66-118 with src/agent/one_step_agent.rs:53-86, eval interleave
- * on) on host cores: `threads` independent env+agent pairs, one per thread,
- * no sharing — the reference itself is single-threaded.
+ * Times the oracle's faithful single-env restatement of the reference training
+ * loop (src/agent.rs:66-118 with src/agent/one_step_agent.rs:53-86; dense-array
+ * Q, no per-step history Vecs) on host cores: `threads` independent env+agent
+ * pairs, one per thread, no sharing — the reference itself is single-threaded
+ * (SURVEY §5).  The eval interleave (src/agent.rs:107-113) runs when eval_at > 0
+ * (the bins pass n/10).  Each thread trains `repeats` fresh agents of
+ * n_episodes each.  The reference's own data structures (FxHashMap Q etc.)
+ * are timed by ref_faithful.c ("ref_faithful").
  *
  * usage: rlref_bench <env> <map8x8> <slippery> <agent> <policy> <selector> <algo>
- *                    <n_episodes> <eval_at> <threads>
+ *                    <n_episodes> <eval_at> <threads> [repeats]
  * prints one JSON line: {"steps":..,"seconds":..,"threads":..,"steps_per_sec":..}
  */
 #include "rlref.h"
@@ -18,13 +22,17 @@
 
 typedef struct {
     rlo_config c;
-    uint64_t n_episodes, eval_at, steps;
+    uint64_t n_episodes, eval_at, steps, repeats;
     double seconds;
 } job;
 
 static void *run(void *p) {
     job *j = (job *)p;
-    j->steps = rlo_faithful_bench(&j->c, j->n_episodes, j->eval_at, &j->seconds);
+    for (uint64_t k = 0; k < j->repeats; ++k) {
+        double sec = 0.0;
+        j->steps += rlo_faithful_bench(&j->c, j->n_episodes, j->eval_at, &sec);
+        j->seconds += sec;
+    }
     return NULL;
 }
 
@@ -40,6 +48,7 @@ int main(int argc, char **argv) {
     uint64_t n = strtoull(argv[8], NULL, 10), eval_at = strtoull(argv[9], NULL, 10);
     int threads = atoi(argv[10]);
     if (threads < 1) threads = 1;
+    const uint64_t repeats = argc > 11 ? strtoull(argv[11], NULL, 10) : 1;
     /* CLI defaults of the reference bins: src/bin/frozen_lake.rs:35-73,84 */
     c.max_steps = 100; c.lr = 0.05; c.gamma = 0.95; c.lambda_ = 0.5; c.eps0 = 1.0;
     c.eps_decay = 1.0 / (0.5 * (double)n); c.eps_final = 0.0; c.ucb_c = 0.5; c.q_default = 0.0;
@@ -53,6 +62,7 @@ int main(int argc, char **argv) {
         jobs[i].c.lane_offset = (uint64_t)i;
         jobs[i].n_episodes = n;
         jobs[i].eval_at = eval_at;
+        jobs[i].repeats = repeats;
         pthread_create(&tid[i], NULL, run, &jobs[i]);
     }
     uint64_t steps = 0;
