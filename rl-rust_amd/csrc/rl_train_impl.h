@@ -559,6 +559,17 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                        lay.trc_cap, nthr, tid};
     if constexpr (PAIRS) { if (active) pair_cache_load(p, pc, lane, tcnt); }
 
+    // the A visible-flag bytes of LDS row s of table tbl, one per action (A <= 6:
+    // the row starts at byte A*(tbl*SL + s), at most 2 bytes into its first word,
+    // so two words hold it)
+    constexpr uint64_t row_mask = 0x0707070707070707ull >> (8 * (8 - A));
+    auto row_flags = [&](uint32_t tbl, uint32_t s) -> uint64_t {
+        static_assert(A <= 6, "flag rows span at most two LDS words");
+        const uint32_t off = qi(tbl, s, 0u), w = off >> 2;
+        const uint64_t two = (uint64_t)QF[w] | ((uint64_t)QF[w + 1u] << 32);
+        return (two >> ((off & 3u) * 8u)) & row_mask;
+    };
+    auto flag_nan = [](uint32_t f) -> bool { return (f & QF_NAN) || (f & (QF_PINF | QF_NINF)) == (QF_PINF | QF_NINF); };
     // f64 image of entry idx (exact: |raw| <= 2^51)
     auto val = [&](uint32_t idx, int64_t raw) -> double {
         if constexpr (SPEC) return q_val(raw, QF8[idx] & QF_MASK);
@@ -707,11 +718,29 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
-        load_rows(s2, ra2, rb2);                   // s2 == 0 (a valid row) on idle lanes
+        // UCB + expected SARSA (SPEC): the visible flags of row s2 decide most of
+        // the step without Q values or counters (the regime is mostly
+        // non-finite rows).  u_0 NaN sticks as the argmax (utils.rs:1-11); any
+        // non-finite value in the target row makes some u_i non-finite (v_i, or
+        // v_i + b0 when n_i = 0: inf or NaN either way), so sum(u) is non-finite,
+        // some p_i is NaN and the expectation — and td — are NaN
+        // (upper_confidence_bound.rs:48-63, src/agent.rs:35-45).
+        bool sel_nan0 = false, tgt_nf = false;
+        if constexpr (SPEC) {
+            const uint64_t f0 = row_flags(0u, s2), f1 = P == 2 ? row_flags(1u, s2) : 0ull;
+            sel_nan0 = flag_nan((uint32_t)f0 & 0xffu) || (P == 2 && flag_nan((uint32_t)f1 & 0xffu));
+            tgt_nf = ((((P == 2 && !L.dflag) ? f1 : f0) & row_mask) != 0ull);
+        }
+        const bool train_lane = doS && L.mode == RL_MODE_TRAIN;
+        if (!SPEC || !(sel_nan0 && (tgt_nf || !train_lane))) load_rows(s2, ra2, rb2);   // s2 == 0 on idle lanes
+        else {
+#pragma unroll
+            for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
+        }
 #if RLAMD_EXP & 4   // timing experiment: greedy selection, no RNG (results differ)
         if (alive) { int64_t v[A]; for (int i = 0; i < A; ++i) v[i] = ra2[i]; a2 = argmax_i64<A>(v); }
 #else
-        if (alive) a2 = select(s2, ra2, rb2);
+        if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2);
 #endif
         if constexpr (UCB) {
             __syncthreads();
@@ -741,6 +770,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 fq = q_val(max_i64<A>(rv));                // utils::max on exact images
             } else if constexpr (ALGO == RL_ALGO_SARSA && !SPEC) {
                 fq = q_val(pick<A>(rv, a2));
+            } else if (SPEC && tgt_nf) {
+                fq = __builtin_nan("");
             } else {
                 double q2[A], pr[A];
 #pragma unroll
@@ -772,9 +803,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
                 fq = future_q<ALGO, A>(q2, a2, pr);
             }
-            const uint32_t qidx = qi(vt, L.s, L.a);
-            const double qa = val(qidx, (int64_t)Q[qidx]);
-            td = r + p.gamma * fq - qa;
+            if (SPEC && tgt_nf) {
+                td = __builtin_nan("");                    // r + gamma * NaN - q
+            } else {
+                const uint32_t qidx = qi(vt, L.s, L.a);
+                const double qa = val(qidx, (int64_t)Q[qidx]);
+                td = r + p.gamma * fq - qa;
+            }
         }
         if constexpr (!TRACES) {
             const uint32_t idx = qi(ut, L.s, L.a);
