@@ -416,6 +416,9 @@ int agent_select_kernel(rl_agent *a) {
     a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo,
                          a->priv ? 1 : 0);
     if (!a->fn) return fail(RL_E_ARG, "no kernel for this (env, agent, policy, selector)");
+    if (!a->priv && a->cfg.selector == RL_SEL_UCB && a->cfg.algo == RL_ALGO_EXPECTED_SARSA &&
+        (uint64_t)a->G * a->K >= (1ull << 32))   // a launch's counter increments are u32 per entry
+        return fail(RL_E_ARG, "UCB + expected SARSA: group_size * sync_every must stay below 2^32");
     if (a->priv) {
         a->block = dim3(256);
         a->grid = dim3((a->L + 255) / 256);

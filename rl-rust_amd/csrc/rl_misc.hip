@@ -28,8 +28,8 @@ size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, u
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
                          uint32_t n_start, uint32_t nthr, uint32_t trc_kb) {
     const int traces = agent != RL_AGENT_TRACES ? 0 : layout_sparse_traces(agent, sel, algo, 0) ? 2 : 1;
-    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, sel == RL_SEL_UCB, traces, S, A, n_start, nthr,
-                       trc_kb).total;
+    const int ucb = sel != RL_SEL_UCB ? 0 : algo == RL_ALGO_EXPECTED_SARSA ? 2 : 1;
+    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, ucb, traces, S, A, n_start, nthr, trc_kb).total;
 }
 
 // ---------------------------------------------------------------- lane init

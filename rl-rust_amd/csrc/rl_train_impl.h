@@ -19,7 +19,7 @@
 namespace rlamd {
 
 struct SmemLayout {
-    uint32_t st, q, sum, cnt, qf, n, t, list, rcp, tr, cdf, trc, total;
+    uint32_t st, q, sum, cnt, qf, n, nd, t, list, rcp, tr, cdf, trc, total;
     uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
@@ -75,7 +75,12 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.cnt = off; off += shared_q ? align16(((PSA + 1u) / 2u) * 4u) : 0u;
     l.qf = off; off += (shared_q && ucb) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
-    l.n = off; off += (shared_q && ucb) ? align16(SA * 8u) : 0u;
+    // UCB counters: u64 N[S][A] (ucb == 1); UCB + expected SARSA (ucb == 2): the
+    // launch's own increments u32 NL[S][A] over the HBM base plus this step's
+    // increments u16 D[S][A] (rl_train_impl.h train_shared_body, SPEC)
+    l.n = off;
+    l.nd = off + align16(SA * 4u);
+    off += (shared_q && ucb) ? (ucb == 2 ? align16(SA * 4u) + align16(((SA + 1u) / 2u) * 4u) : align16(SA * 8u)) : 0u;
     l.t = off; off += (shared_q && ucb) ? 16u : 0u;
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
     l.rcp = off; off += align16(l.nrcp * 8u);
@@ -482,7 +487,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     constexpr bool PAIRS = TRACES && !SPEC;            // layout_sparse_traces (rl_kparams.h)
-    const SmemLayout lay = smem_layout(ENV, P, UCB, TRACES ? (PAIRS ? 2 : 1) : 0, S, A, p.n_start, nthr, p.trc_kb);
+    const SmemLayout lay = smem_layout(ENV, P, UCB ? (SPEC ? 2 : 1) : 0, TRACES ? (PAIRS ? 2 : 1) : 0, S, A, p.n_start,
+                                       nthr, p.trc_kb);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // two u16 counters per word
@@ -491,6 +497,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint8_t *QF8 = (uint8_t *)(smem + lay.qf);
     unsigned long long *N = (unsigned long long *)(smem + lay.n);
     unsigned long long *T = (unsigned long long *)(smem + lay.t);
+    // SPEC counters: n = n_base (HBM, u64) + NL (this launch) [+ D (this step)]
+    uint32_t *NL = (uint32_t *)(smem + lay.n);
+    uint32_t *D32 = (uint32_t *)(smem + lay.nd);
+    uint16_t *D16 = (uint16_t *)(smem + lay.nd);
     uint16_t *LIST = (uint16_t *)(smem + lay.list);
     uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSAL * 2u));
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
@@ -528,8 +538,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < PSA; i += nthr) QF8[lds_of(i)] = (uint8_t)p.qf_base[i];
-        for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = (unsigned long long)p.n_base[i];
-        if (tid == 0) T[0] = p.t_base[0];
+        if constexpr (SPEC) {
+            for (uint32_t i = tid; i < SA; i += nthr) NL[i] = 0u;
+            for (uint32_t i = tid; i < (SA + 1u) / 2u; i += nthr) D32[i] = 0u;
+        } else {
+            for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = (unsigned long long)p.n_base[i];
+        }
+        if (tid == 0) { T[0] = p.t_base[0]; T[1] = 0ull; }
     }
     if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
@@ -552,8 +567,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // increments between a step's selection and its probabilities, so the
     // probabilities' ln(t_{k+1}) is also step k+1's selection value.
     constexpr bool ESU = UCB && ALGO == RL_ALGO_EXPECTED_SARSA;
+    // computed lazily (only lanes whose row needs the UCB values pay for the log;
+    // in the all-NaN regime no wave does), then reused until the next increments
     double lnt_es = 0.0;
-    if constexpr (ESU) lnt_es = rl_log((double)T[0]);
+    bool lnt_ok = false;
+    auto lnt_cur = [&](unsigned long long t) -> double {
+        if (!lnt_ok) { lnt_es = rl_log((double)t); lnt_ok = true; }
+        return lnt_es;
+    };
+    // visit count of (s, i) as the reference's u128 counter: the step-start value
+    // (selection) or with this step's increments (expected SARSA's probabilities)
+    auto ucount = [&](uint32_t s, uint32_t i, bool with_step) -> uint64_t {
+        const uint32_t idx = qi(0u, s, i);
+        if constexpr (SPEC)
+            return p.n_base[s * (uint32_t)A + i] + (uint64_t)NL[idx] + (with_step ? (uint64_t)D16[idx] : 0ull);
+        else return N[idx];
+    };
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
     const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * nthr * 2u)),
                        lay.trc_cap, nthr, tid};
@@ -613,12 +642,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         } else {                                    // upper_confidence_bound.rs:29-42
             double u[A], v[A];
             uint64_t n[A];
-            const double lnt = ESU ? lnt_es : rl_log((double)T[0]);
+            const double lnt = ESU ? lnt_cur(T[0]) : rl_log((double)T[0]);
 #pragma unroll
             for (int i = 0; i < A; ++i) {
                 v[i] = val(qi(0, s, i), ra[i]);
                 if constexpr (P == 2) v[i] = (v[i] + val(qi(1, s, i), rb[i])) / 2.0;
-                n[i] = N[qi(0, s, i)];
+                n[i] = ucount(s, (uint32_t)i, false);
             }
             uint32_t need = ucb_known<A>(v, n, p.ucb_c, lnt, u);
             // argmax (utils.rs:1-11) is decided without the unknown (finite) values
@@ -742,18 +771,25 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #else
         if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2);
 #endif
-        if constexpr (UCB) {
+        uint32_t d_own = 0xffffffffu;   // SPEC: the D entry this lane settles at step end
+        if constexpr (SPEC) {
+            // the step's increments go to D / T[1], apart from what this step's
+            // selections read (NL, T[0]), so no barrier separates the two; expected
+            // SARSA's probabilities read n + D and T[0] + T[1] after the barrier
+            if (alive) {
+                const uint32_t idx = qi(0, s2, a2), sh = (idx & 1u) * 16u;
+                if (((atomicAdd(&D32[idx >> 1], 1u << sh) >> sh) & 0xffffu) == 0u) d_own = idx;
+            }
+            const uint32_t c = (uint32_t)__popcll(__ballot(alive));
+            if ((tid & 63u) == 0 && c) atomicAdd(&T[1], (unsigned long long)c);
+            __syncthreads();
+            lnt_ok = false;   // this step's probabilities and the next selection use ln(T_{k+1})
+        } else if constexpr (UCB) {
             __syncthreads();
             if (alive) atomicAdd(&N[qi(0, s2, a2)], 1ull);
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
-            // only expected SARSA's probabilities read the incremented counters in
-            // this step; otherwise the next reader is the next step's selection,
-            // after the end-of-step barrier
-            if constexpr (ESU) {
-                __syncthreads();
-                lnt_es = rl_log((double)T[0]);   // this step's probabilities and the next selection
-            }
+            // the next reader is the next step's selection, after the end-of-step barrier
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
@@ -779,10 +815,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
-                    const double lnt = lnt_es;
+                    const double lnt = lnt_cur(T[0] + T[1]);
                     uint64_t n[A];
 #pragma unroll
-                    for (int i = 0; i < A; ++i) n[i] = N[qi(0, s2, i)];
+                    for (int i = 0; i < A; ++i) n[i] = ucount(s2, (uint32_t)i, true);
                     uint32_t need = ucb_known<A>(q2, n, p.ucb_c, lnt, pr);
                     // a known non-finite u makes the sum non-finite, so some p_i is
                     // inf/inf or NaN and the expectation is NaN: skip the rest
@@ -945,6 +981,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if (tid == 0) LISTN[0] = 0u;
             }
         }
+        if constexpr (SPEC) {                     // fold the step's counter increments
+            if (d_own != 0xffffffffu) { NL[d_own] += (uint32_t)D16[d_own]; D16[d_own] = 0; }
+            if (tid == 0) { T[0] += T[1]; T[1] = 0ull; }
+        }
         __syncthreads();   // Q_{t+1} complete before the next step's reads
         bool tr = false, ev = false;
         if (doS) {
@@ -1010,7 +1050,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < SA; i += nthr) {
-            const int64_t d = (int64_t)(N[lds_of(i)] - (unsigned long long)p.n_base[i]);
+            const int64_t d = SPEC ? (int64_t)NL[i] : (int64_t)(N[lds_of(i)] - (unsigned long long)p.n_base[i]);
             if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + i], (unsigned long long)d);
         }
         if (tid == 0) {
