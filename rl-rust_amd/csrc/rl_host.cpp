@@ -584,28 +584,39 @@ double env_reward_bound(int kind) {
 // Mb = max(|Q_0|, R/(1-gamma)), and every delta within lr*E*(R + (1+gamma)Mb).
 // UCB + expected SARSA weighs by u_i / sum(u) (upper_confidence_bound.rs:48-63):
 // no bound, its kernels always count.
-bool hits_proven_zero(const rl_agent *a) {
+// Returns the proven bound on |lr * E * td| (+inf when nothing is proven); the
+// clamp and the delta saturation provably never engage when it is < 2000.
+double delta_bound(const rl_agent *a) {
+    const double inf = std::numeric_limits<double>::infinity();
     const rl_agent_config &c = a->cfg;
-    if (a->priv || a->neural) return false;
-    if (c.selector == RL_SEL_UCB && c.algo == RL_ALGO_EXPECTED_SARSA) return false;
+    if (a->priv || a->neural) return inf;
+    if (c.selector == RL_SEL_UCB && c.algo == RL_ALGO_EXPECTED_SARSA) return inf;
     const double lr = c.lr, g = c.gamma;
-    if (!(lr >= 0.0 && g >= 0.0 && g < 1.0 && std::isfinite(a->q_abs0))) return false;
+    if (!(lr >= 0.0 && g >= 0.0 && g < 1.0 && std::isfinite(a->q_abs0))) return inf;
     double emax = 1.0;
     if (c.agent == RL_AGENT_TRACES) {
         const double gl = g * c.lambda;
-        if (!(gl >= 0.0 && gl < 1.0)) return false;
+        if (!(gl >= 0.0 && gl < 1.0)) return inf;
         emax = 1.0 / (1.0 - gl);
     }
-    if (!(lr * emax <= 1.0)) return false;
+    if (!(lr * emax <= 1.0)) return inf;
     if (c.selector == RL_SEL_EPS_GREEDY && c.algo == RL_ALGO_EXPECTED_SARSA) {
         // eps stays in [eps_final, eps0] (or decays toward 0 by a factor in [0,1])
         const bool dec = c.decay_kind == RL_DECAY_MUL ? (c.eps_decay >= 0.0 && c.eps_decay <= 1.0) : c.eps_decay >= 0.0;
-        if (!(c.eps0 >= 0.0 && c.eps0 <= 1.0 && c.eps_final >= 0.0 && dec)) return false;
+        if (!(c.eps0 >= 0.0 && c.eps0 <= 1.0 && c.eps_final >= 0.0 && dec)) return inf;
     }
     const double R = env_reward_bound(c.env.kind);
     const double mb = std::max(a->q_abs0, R / (1.0 - g));
-    return mb <= 2000.0 && lr * emax * (R + (1.0 + g) * mb) < 2000.0;
+    if (!(mb <= 2000.0)) return inf;
+    return lr * emax * (R + (1.0 + g) * mb);
 }
+bool hits_proven_zero(const rl_agent *a) { return delta_bound(a) < 2000.0; }
+// The 8-wave kernels pack a step's contributions to an entry into one int64,
+// sum * 2^11 + count (one LDS atomic per contribution instead of two): exact
+// while at most G contributions of at most delta_bound * 2^40 + 1 raw units each
+// keep |sum| * 2^11 + 2047 below 2^63, i.e. G * delta_bound < 2^12 (FrozenLake and
+// Blackjack at the CLI defaults: 0.15 * 512 and 2.0 * 512)
+bool pack_proven(const rl_agent *a) { return (double)a->G * delta_bound(a) < 4000.0; }
 
 void agent_sync_params(rl_agent *a) {
     KParams &p = a->kp;
@@ -618,6 +629,7 @@ void agent_sync_params(rl_agent *a) {
     p.decay_kind = a->cfg.decay_kind;
     p.algo = a->cfg.algo;
     p.hits_zero = hits_proven_zero(a) ? 1 : 0;
+    p.pack_ok = p.hits_zero && pack_proven(a) ? 1 : 0;
     p.delta = a->delta;
     p.plan_steps = a->plan;
     p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;

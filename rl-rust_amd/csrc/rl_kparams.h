@@ -96,6 +96,9 @@ struct KParams {
     // the throughput kernels then skip counting rl_stats::q_clamp_hits /
     // delta_saturations (both provably 0)
     int32_t hits_zero;
+    // ... and that a step's contributions to an entry fit one int64 as sum * 2^11 +
+    // count (rl_host.cpp pack_proven): the 8-wave kernels then use one LDS atomic each
+    int32_t pack_ok;
     // train()/evaluate() control
     uint64_t target_episodes, eval_at;
     uint64_t eval_div;     // ceil(2^64 / eval_at) (mod 2^64): divisibility test constant

@@ -472,7 +472,7 @@ __device__ __forceinline__ void fold_flags(uint8_t *QF8, uint32_t idx) {
 // HITS: count clamp hits / delta saturations (off only where the host proved both 0:
 // KParams::hits_zero)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1,
-          bool HITS = true>
+          bool HITS = true, bool PACK = false>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -664,7 +664,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // counter add needs no return value.  Owner form: the step's first
     // contributor (old count 0) settles the entry.
     const bool sweep = SWEEP == 1 || PSAL <= nthr;   // SWEEP == 1: the host checked PSA <= block
+    // PACKC: one LDS atomic per contribution — SUM[idx] holds sum * 2^11 + count
+    // (KParams::pack_ok: the host proved |sum| * 2^11 + 2047 < 2^63)
+    constexpr bool PACKC = PACK && !SPEC && !TRACES;
     auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
+        if constexpr (PACKC) {
+            const unsigned long long v = (unsigned long long)(sum * 2048) + n;
+            if (sweep) { atomicAdd(&SUM[idx], v); return false; }
+            return (atomicAdd(&SUM[idx], v) & 2047ull) == 0ull;
+        }
         const uint32_t sh = (idx & 1u) * 16u;
         bool first = false;
         if (sweep) atomicAdd(&CNT[idx >> 1], n << sh);
@@ -677,14 +685,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // accumulators; returns whether the clamp engaged (counted by the caller with
     // a wave ballot after reconvergence: no branch, no VGPR)
     auto settle = [&](uint32_t idx) -> bool {
-        const uint32_t n = CNT16[idx];
-        const int64_t sum = (int64_t)SUM[idx];
+        const int64_t packed = (int64_t)SUM[idx];
+        const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[idx];
+        const int64_t sum = PACKC ? (packed >> 11) : packed;
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
         bool hit = false;
         if constexpr (HITS) Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
         else Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
         SUM[idx] = 0ull;
-        CNT16[idx] = 0;
+        if constexpr (!PACKC) CNT16[idx] = 0;
         if constexpr (SPEC) fold_flags(QF8, idx);
         return hit;
     };
@@ -1082,9 +1091,17 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // the host proved both counts 0 (KParams::hits_zero), else k_train_shared.
 template <int SEL, int ALGO>
 constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA; }
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, bool PACK>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>()>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>(), PACK>(p);
+}
+// the 8-wave kernel for (SLIP, SWEEP), packed contributions when the host proved them exact
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
+const void *o8_kernel(const KParams &p) {
+    if constexpr (!o8_counts_hits<SEL, ALGO>()) {
+        if (p.pack_ok) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, true>;
+    }
+    return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, false>;
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
@@ -1340,13 +1357,13 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
             // owned by one thread when P*S*A <= block size) as compile-time constants
             const bool sw = p.P * p.S * p.A <= block.x;
             if constexpr (ENV == RL_ENV_FROZEN_LAKE) {
-                if (!p.slippery) k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0, 1>
-                                        : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 0, -1>;
-                else k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1, 1>
-                            : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, 1, -1>;
+                if (!p.slippery) k = sw ? o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, 0, 1>(p)
+                                        : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, 0, -1>(p);
+                else k = sw ? o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, 1, 1>(p)
+                            : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, 1, -1>(p);
             } else {
-                k = sw ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>
-                       : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>;
+                k = sw ? o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>(p)
+                       : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>(p);
             }
           } else {
             k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;

@@ -12,7 +12,7 @@ wait
 for m in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o exp/librlamd_$m.so exp/fl_$m.o \
      build/rl_train_cliff_walking.hip.o build/rl_train_taxi.hip.o build/rl_train_blackjack.hip.o \
-     build/rl_train_frozen_lake_edited.hip.o build/rl_misc.hip.o build/rl_host.cpp.o
+     build/rl_train_frozen_lake_edited.hip.o build/rl_misc.hip.o build/rl_host.cpp.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 done
 rm -f exp/*.o
 ls -la exp
