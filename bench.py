@@ -53,6 +53,9 @@ def parse():
     for k in ("env", "agent", "policy", "selector", "algo"):
         ap.add_argument("--" + k, default=None)
     ap.add_argument("--map8x8", type=int, default=1)
+    ap.add_argument("--reset-step", type=int, default=None,
+                    help="batched schedule: resetting lanes also step in the same synchronous step "
+                         "(rl_agent_set_reset_step; eps-greedy)")
     ap.add_argument("--slippery", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,8 +63,10 @@ def parse():
                     help="PMC summaries per workload (scripts/collect_counters.py)")
     a = ap.parse_args()
     for k, v in PRESETS[a.config].items():
-        if getattr(a, k) is None:
+        if k != "reset_step" and getattr(a, k) is None:
             setattr(a, k, v)
+    if a.reset_step is None:
+        a.reset_step = PRESETS[a.config].get("reset_step", 0)
     return a
 
 
@@ -71,10 +76,13 @@ PRESETS = {
             algo="qlearning", lanes=1 << 20, group=512),
     3: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="expected_sarsa",
             lanes=1 << 20, group=512),
+    # cfg 4 / 5: the reset-and-step schedule (short episodes: a reset no longer costs
+    # a synchronous step; measured 7.03e9 -> 7.25e9 and 5.94e10 -> 8.68e10; on cfg 2,
+    # where 3 % of lane-steps are resets, the second selection costs more: 0.84x)
     4: dict(env="cliff_walking", agent="traces", policy="tabular", selector="eps_greedy", algo="sarsa",
-            lanes=1 << 17, group=256),
+            lanes=1 << 17, group=256, reset_step=1),
     5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
-            lanes=1 << 19, group=512),
+            lanes=1 << 19, group=512, reset_step=1),
 }
 
 
@@ -192,6 +200,8 @@ def main():
                              sync_every=args.sync, lane_offset=rank * args.lanes,
                              device=dev)
     agent = rlamd.Agent(p)
+    if args.reset_step:
+        agent.set_reset_step(True)
     occ = agent.occupancy()   # resident learner groups per CU (LDS / VGPR limited)
     stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
     torch.cuda.set_stream(stream)
@@ -269,7 +279,8 @@ def main():
                                f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
-                   "survey_cfg": args.config, "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
+                   "survey_cfg": args.config,
+                   "schedule": "reset-and-step" if args.reset_step else "one action per synchronous step", "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
                    "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"

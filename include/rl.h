@@ -128,6 +128,8 @@ typedef struct rl_agent_config {
  *   kind 1 RESET: s = Env::reset(), a = get_action(s)              (s, a set)
  *   kind 2 STEP:  (s2, r, term) = Env::step(a), a2 = get_action(s2), update;
  *                 td is the value pushed to training_error (src/agent.rs:98)
+ *   kind 3 RESET + STEP (rl_agent_set_reset_step): s = Env::reset(), a =
+ *                 get_action(s), then kind 2 from (s, a)
  *   kind 0: lane idle (finished its train()/evaluate() call)
  * For Blackjack s/s2 are dense indices (see rl_obs_to_reference). */
 typedef struct rl_step_record {
@@ -244,6 +246,15 @@ int rl_agent_dims(rl_agent *a, uint32_t *n_states, uint32_t *n_actions, uint32_t
  * planning after every training update; 0 = the plain agent.  Private mode
  * (group_size 1) only; the model is emptied here and by rl_agent_reset. */
 int rl_agent_set_planning(rl_agent *a, uint32_t planning_steps);
+/* Batched-schedule option (shared mode, eps-greedy selection; no reference
+ * counterpart — the reference has one env): off (default), a lane that needs a
+ * reset spends a synchronous step on env.reset() + get_action (kind 1 record);
+ * on, it resets, selects AND steps in the same synchronous step (one kind 3
+ * record: a STEP whose (s, a) came from the reset), both selections reading the
+ * step's Q snapshot.  Each lane still runs the reference loop (src/agent.rs:80-106)
+ * in order; worth it where episodes are short (Blackjack: ~40 % of lane-steps
+ * are resets).  Ignored in private mode and with UCB. */
+int rl_agent_set_reset_step(rl_agent *a, int32_t enable);
 /* episode log (device-side reward_history / episode_length, src/agent.rs:72-141):
  * a ring of `capacity_per_lane` records per lane ([slot][lane] in HBM); 0 disables.
  * Enabling (re)allocates and empties the log. */

@@ -1335,6 +1335,7 @@ struct rlo_batch {
     vec records;
     uint64_t stats[16];  /* rl_stats order; 8 = Q clamp hits, 9 = delta saturations */
     uint32_t plan;       /* Dyna planning steps per update (private mode only) */
+    int reset_step;      /* reset-and-step schedule (shared mode, eps-greedy) */
     netdef net;          /* NeuralPolicy (private mode only) */
     double *feat, *w_g;  /* input features [S][in]; current lane's parameters */
     uint32_t net_gen;
@@ -1504,6 +1505,7 @@ void rlo_batch_reset(rlo_batch *b) {
         L->model.cnt = 0;                    /* model.reset (internal_model_agent.rs:79-82) */
     }
 }
+void rlo_batch_set_reset_step(rlo_batch *b, int on) { b->reset_step = on != 0; }
 int rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps) {
     if (planning_steps && !b->priv) return -1;   /* Dyna: private agents only */
     b->plan = planning_steps;
@@ -1636,7 +1638,15 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
         lane_t *L = &b->lanes[lane0 + j];
         kind[j] = 0;
         if (L->mode == RLO_MODE_DONE) continue;
-        if (L->need_reset) {
+        if (L->need_reset && b->reset_step && !b->priv && !ucb) {
+            /* reset-and-step schedule: env.reset() + get_action against the
+             * snapshot, then the step from (s0, a0) (src/agent.rs:83-89) */
+            kind[j] = 3;
+            L->s = env_reset(&b->E, &L->st, &L->rng);
+            L->a = b_select(b, L, L->s);
+            L->need_reset = 0; L->epi_reward = 0.0; L->epi_len = 0;
+            if (env_step(&b->E, &L->st, L->a, &L->rng, &s2v[j], &rv[j], &tv[j])) abort();
+        } else if (L->need_reset) {
             kind[j] = 1;
             s2v[j] = env_reset(&b->E, &L->st, &L->rng);
             rv[j] = 0.0; tv[j] = 0;

@@ -186,6 +186,9 @@ void   rlo_batch_set_selector(rlo_batch *b, int32_t selector);
 void   rlo_batch_set_algo(rlo_batch *b, int32_t algo);
 /* Dyna planning steps per update (private mode only; -1 otherwise) */
 int    rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps);
+/* batched schedule option: a lane needing a reset resets, selects (snapshot) and
+ * steps in the same synchronous step (record kind 3); shared mode, eps-greedy */
+void   rlo_batch_set_reset_step(rlo_batch *b, int on);
 
 #ifdef __cplusplus
 }

@@ -1360,6 +1360,12 @@ int rl_agent_take_records(rl_agent *a, rl_step_record *out, uint64_t cap, uint64
     return RL_OK;
 }
 
+int rl_agent_set_reset_step(rl_agent *a, int32_t enable) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    a->kp.reset_step = enable ? 1 : 0;
+    return RL_OK;
+}
+
 int rl_agent_set_planning(rl_agent *a, uint32_t planning_steps) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (planning_steps && !a->priv) return fail(RL_E_ARG, "Dyna planning needs group_size 1 (private agents)");

@@ -99,6 +99,9 @@ struct KParams {
     // ... and that a step's contributions to an entry fit one int64 as sum * 2^11 +
     // count (rl_host.cpp pack_proven): the 8-wave kernels then use one LDS atomic each
     int32_t pack_ok;
+    // batched schedule option (rl_agent_set_reset_step; shared mode, eps-greedy):
+    // a lane that needs a reset resets, selects and steps in one synchronous step
+    int32_t reset_step;
     // train()/evaluate() control
     uint64_t target_episodes, eval_at;
     uint64_t eval_div;     // ceil(2^64 / eval_at) (mod 2^64): divisibility test constant

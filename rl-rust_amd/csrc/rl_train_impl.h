@@ -733,13 +733,34 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         // (env.reset() + get_action, src/agent.rs:83-84) or STEPs (env.step +
         // get_action + update, :88-97); one selection per lane per step.
         const bool alive = L.mode != RL_MODE_DONE;
-        const bool doR = alive && L.need_reset;
-        const bool doS = alive && !L.need_reset;
+        bool doR = alive && L.need_reset;
+        bool doS = alive && !L.need_reset;
         const uint32_t mode_before = L.mode;
         uint32_t s2 = 0, a2 = 0;
         double r = 0.0;
         bool term = false;
         int64_t ra2[A], rb2[A];
+        // reset-and-step schedule (KParams::reset_step, eps-greedy only): a lane
+        // that needs a reset does env.reset() + get_action against the step
+        // snapshot and then steps in the same synchronous step
+        bool fused = false;
+        if constexpr (!UCB) {
+            if (p.reset_step) {
+                if (doR) {
+                    const uint32_t s0 = E::reset(L.z, L.rng, tabs);
+                    L.ready = true;
+                    load_rows(s0, ra2, rb2);
+                    L.a = select(s0, ra2, rb2);
+                    L.s = s0;
+                    L.need_reset = false;
+                    L.epi_reward = 0.0;
+                    L.epi_len = 0;
+                    fused = true;
+                }
+                doR = false;
+                doS = alive;
+            }
+        }
         if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED) {
             uint32_t pos = L.s;                    // reset or step in one predicated block
             fl_advance<ENV == RL_ENV_FROZEN_LAKE_EDITED, SLIP, LDS_AM>(doR, doS, pos, L.z, L.a, L.rng, tabs, s2, r,
@@ -1001,7 +1022,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
                 if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
             }
-            if (INSTR && p.rec) write_record(p, k, lane, 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
+            if (INSTR && p.rec) write_record(p, k, lane, fused ? 3u : 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
             if (tr) atomicAdd(RSUM, (unsigned long long)(int64_t)__builtin_rint(L.epi_reward * 65536.0));
             if (INSTR && p.elog && (tr || ev)) log_episode(p, lane, L, tr);

@@ -111,6 +111,7 @@ SIGNATURES = {
     "rl_agent_take_records": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64)]),
     "rl_agent_set_episode_log": (C.c_int, [_V, C.c_uint32]),
     "rl_agent_set_planning": (C.c_int, [_V, C.c_uint32]),
+    "rl_agent_set_reset_step": (C.c_int, [_V, C.c_int32]),
     "rl_agent_take_episodes": (C.c_int, [_V, _V, C.c_uint64, _P(C.c_uint64), _P(C.c_uint64)]),
     "rl_agent_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
     "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
@@ -370,6 +371,11 @@ class Agent:
         out = np.zeros(n.value, RECORD_DTYPE)
         check(lib().rl_agent_take_records(self.h, out.ctypes.data, n.value, C.byref(n)))
         return out.reshape(-1, self.L)
+
+    def set_reset_step(self, on=True):
+        """batched schedule: a resetting lane also steps in the same synchronous step
+        (shared mode, eps-greedy; rl.h rl_agent_set_reset_step)"""
+        check(lib().rl_agent_set_reset_step(self.h, int(on)))
 
     def set_planning(self, planning_steps):
         """InternalModelAgent + RandomModel (Dyna-Q); private mode only."""

@@ -1,7 +1,8 @@
 """Full-size golden fixtures (VERDICT r01 "next" 2): the oracle's batched
 schedule at the EXACT configurations bench.py measures (SURVEY §8(d) cfg 2-5,
 plus the slippery cfg 2 variant): per-GPU lane counts, learner-group sizes,
-K = 64 and the reference CLI's default ε schedule (n_episodes 1e5,
+K = 64, the batched schedule bench.py uses (reset-and-step for cfg 4 / 5) and
+the reference CLI's default ε schedule (n_episodes 1e5,
 src/bin/frozen_lake.rs:35-73,84), two launches (128 synchronous steps of every
 lane, two merges).  Stored: raw fixed-point Q, a SHA-256 of Q as f64 bits
 (covers the NaN/±inf flags of cfg 3), UCB counters and t, stats (clamp and
@@ -40,7 +41,8 @@ def bench_params(cfg, extra):
     import bench
     pr = dict(bench.PRESETS[cfg])
     kw = dict(env=pr["env"], agent=pr["agent"], policy=pr["policy"], selector=pr["selector"],
-              algo=pr["algo"], n_lanes=pr["lanes"], group_size=pr["group"], sync_every=SYNC)
+              algo=pr["algo"], n_lanes=pr["lanes"], group_size=pr["group"], sync_every=SYNC,
+              reset_step=pr.get("reset_step", 0))
     if pr["env"] == "frozen_lake":
         kw["map8x8"] = 1
     kw.update(extra)
@@ -59,7 +61,8 @@ def case(name):
     import oracle_ffi as O
     cfg, extra = CASES[name]
     kw = bench_params(cfg, extra)
-    b = O.Batch(O.default_params(**kw))
+    b = O.Batch(O.default_params(**{k: v for k, v in kw.items() if k != "reset_step"}))
+    b.set_reset_step(bool(kw["reset_step"]))
     b.run(LAUNCHES)
     out = {"survey_cfg": cfg, "params": kw, "launches": LAUNCHES,
            "q_raw_i64_b64": b64(b.q_raw().astype("<i8")),

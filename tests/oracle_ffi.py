@@ -44,7 +44,7 @@ class Config(C.Structure):
 RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
                          ("term", "u1"), ("mode", "u1"), ("kind", "u1"), ("pad", "u1", (3,)),
                          ("r", "<f8"), ("td", "<f8")])
-KIND_IDLE, KIND_RESET, KIND_STEP = 0, 1, 2
+KIND_IDLE, KIND_RESET, KIND_STEP, KIND_RESET_STEP = 0, 1, 2, 3
 assert RECORD_DTYPE.itemsize == 32
 
 
@@ -107,6 +107,7 @@ def lib():
         L.rlo_gen_index_u64.restype = C.c_uint64
         L.rlo_gen_index_u64.argtypes = [C.c_uint64, C.c_uint64, P(C.c_int)]
         L.rlo_faithful_set_planning.argtypes = [C.c_void_p, C.c_uint32]
+        L.rlo_batch_set_reset_step.argtypes = [C.c_void_p, C.c_int]
         L.rlo_batch_set_planning.restype = C.c_int
         L.rlo_batch_set_planning.argtypes = [C.c_void_p, C.c_uint32]
         L.rlo_uniform_card_u32.restype = C.c_uint32
@@ -387,6 +388,9 @@ class Batch:
 
     def set_planning(self, n):
         assert lib().rlo_batch_set_planning(self.h, n) == 0, "Dyna planning needs group_size 1"
+
+    def set_reset_step(self, on=True):
+        lib().rlo_batch_set_reset_step(self.h, int(on))
 
     @property
     def private(self):

@@ -41,7 +41,8 @@ def test_bench_config_matches_fullsize_fixture(rl, name):
     cfg, extra = CASES[name]
     kw = bench_params(cfg, extra)
     assert kw == g["params"], "bench.py presets moved: regenerate tests/golden/fullsize.json"
-    dev = rl.Agent(rl.default_params(**kw))
+    dev = rl.Agent(rl.default_params(**{k: v for k, v in kw.items() if k != "reset_step"}))
+    dev.set_reset_step(bool(kw["reset_step"]))
     dev.run(g["launches"])
     want = np.frombuffer(base64.b64decode(g["q_raw_i64_b64"]), "<i8")
     got = dev.q_raw().reshape(-1)

@@ -570,3 +570,40 @@ def test_neural_weights_roundtrip_and_dyna(rl, oracle):
     dw, rw = dev.weights(), ref.weights()   # NaN payloads differ between gfx950 and x86: NaN-aware
     assert ((dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))).all()
     _assert_stats_equal(dev, ref)
+
+
+RESET_STEP_CASES = [
+    dict(env="blackjack", policy="double", algo="qlearning", group_size=128),   # cfg 5's kernel (o8)
+    dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64),    # cfg 4's kernel
+    dict(env="frozen_lake", map8x8=1, algo="qlearning", group_size=256),       # o8, sweep form
+    dict(env="taxi", algo="expected_sarsa", group_size=100),
+    dict(env="frozen_lake", map8x8=1, slippery=1, agent="traces", policy="double", algo="expected_sarsa",
+         group_size=64),
+]
+
+
+@pytest.mark.parametrize("case", RESET_STEP_CASES, ids=lambda c: "-".join(f"{v}" for v in c.values()))
+def test_reset_step_schedule_matches_oracle(rl, oracle, case):
+    """rl_agent_set_reset_step: a resetting lane resets, selects and steps in one
+    synchronous step (kind 3 records) — device == oracle bit for bit, in run mode
+    and with the eval interleave."""
+    L = 500
+    p = _params(rl, n_lanes=L, sync_every=16, n_episodes_for_decay=40, **case)
+    dev = rl.Agent(p)
+    dev.set_reset_step(True)
+    dev.set_recording(True)
+    ref = oracle.Batch(p)
+    ref.set_reset_step(True)
+    ref.set_record(True)
+    dev.run(5)
+    ref.run(5)
+    recs = dev.records()
+    _assert_records_equal(recs, ref.records())
+    assert (recs["kind"] == 3).any() and not (recs["kind"] == 1).any()
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+    dev.train(10, 4)
+    ref.train_episodes(10, 4)
+    _assert_records_equal(dev.records(), ref.records())
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)

@@ -234,3 +234,29 @@ def test_train_then_run_keeps_training_oracle(oracle):
     s0 = int(b.stats()[0])
     b.run(2)
     assert int(b.stats()[0]) > s0
+
+
+def test_reset_step_schedule_is_the_reference_loop_per_lane(oracle):
+    """Reset-and-step schedule (oracle/rlref.c, rl_agent_set_reset_step): every
+    synchronous step of a live lane is an Env::step; a kind-3 record starts an
+    episode (its s is the start state, src/env/frozen_lake.rs:106-113) and follows
+    the lane's previous terminal step; run mode steps every lane K times per launch."""
+    p = oracle.default_params(env="frozen_lake", map8x8=1, n_lanes=300, group_size=64, sync_every=20)
+    b = oracle.Batch(p)
+    b.set_reset_step(True)
+    b.set_record(True)
+    b.run(3)
+    recs = b.records()
+    assert set(np.unique(recs["kind"])) <= {oracle.KIND_STEP, oracle.KIND_RESET_STEP}
+    assert (recs["s"][recs["kind"] == oracle.KIND_RESET_STEP] == 0).all()
+    assert b.stats()[0] == 3 * 20 * 300
+    for lane in range(0, 300, 37):
+        r = recs[:, lane]
+        starts = r["kind"] == oracle.KIND_RESET_STEP
+        # an episode starts at step 0 or right after a terminal step, and only there
+        prev_term = np.concatenate([[True], r["term"][:-1] == 1])
+        assert np.array_equal(starts, prev_term)
+        # consecutive steps inside an episode chain s2 -> s, a2 -> a
+        cont = ~starts[1:]
+        assert np.array_equal(r["s"][1:][cont], r["s2"][:-1][cont])
+        assert np.array_equal(r["a"][1:][cont], r["a2"][:-1][cont])
