@@ -328,6 +328,10 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // the 8-wave kernel), so off
 #define RLAMD_BJ_ONE_LOOP 0
 #endif
+#ifndef RLAMD_SWEEP_U
+#define RLAMD_SWEEP_U 4   // pair-trace sweep: rounds of 64 items interleaved per iteration
+                          // (cfg 4: 1 / 2 / 4 -> 1.163 / 1.089 / 1.058 ms per launch)
+#endif
 #ifndef RLAMD_COOP_SWEEP
 #define RLAMD_COOP_SWEEP 1   // shared pair traces: wave-cooperative sweep (0: each lane its own list)
 #endif
@@ -921,41 +925,66 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
                 const uint32_t excl = incl - npl;
                 const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
-                const uint32_t lane_lo = (uint32_t)lane, lane_hi = (uint32_t)(lane >> 32);
                 const uint64_t Ls = p.L;
-                for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
-                    const uint32_t q = q0 + lid;
-                    uint32_t lo = 0;                      // owner: last lane with excl <= q
+                // RLAMD_SWEEP_U rounds per iteration, every stage interleaved across
+                // them (owner searches, gathers, loads, then the updates): with 2
+                // waves per SIMD (cfg 4) the rounds' LDS / HBM round trips overlap
+                // instead of queueing one dependent chain per round
+                constexpr uint32_t U = RLAMD_SWEEP_U;
+                for (uint32_t q0 = 0; q0 < T; q0 += 64u * U) {
+                    uint32_t qv[U], lo[U];
 #pragma unroll
-                    for (uint32_t st = 32; st; st >>= 1) {
-                        const uint32_t e = (uint32_t)__shfl((int)excl, (int)(lo + st), 64);
-                        if (e <= q) lo += st;
-                    }
-                    const uint32_t j = q - (uint32_t)__shfl((int)excl, (int)lo, 64);
-                    const double td_o = __shfl(td, (int)lo, 64);
-                    const uint32_t ut_o = (uint32_t)__shfl((int)ut, (int)lo, 64);
-                    const uint64_t lane_o = (uint64_t)(uint32_t)__shfl((int)lane_lo, (int)lo, 64) |
-                                            ((uint64_t)(uint32_t)__shfl((int)lane_hi, (int)lo, 64) << 32);
-                    if (q < T) {
-                        const uint32_t col = j * nthr + wbase + lo;
-                        const bool in_lds = j < pc.cap;
-                        const uint32_t w = in_lds ? (uint32_t)pc.TRI[col] : (uint32_t)p.tlist[(uint64_t)j * Ls + lane_o];
-                        const double ev = in_lds ? pc.TRE[col] : p.trace[(uint64_t)j * Ls + lane_o];
-                        const uint32_t id = w & 0x7fffu;
-                        const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
-                        if (w & 0x8000u) {                    // the state's row: n += 1
-                            ++trace_states;
-                            const uint32_t rid = ut_o * SL + lrow(o);
-                            if (rsweep) atomicAdd(&CNTR[rid], 1u);
-                            else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+                    for (uint32_t u = 0; u < U; ++u) { qv[u] = q0 + 64u * u + lid; lo[u] = 0; }
+#pragma unroll
+                    for (uint32_t st = 32; st; st >>= 1) {   // owner: last lane with excl <= q
+#pragma unroll
+                        for (uint32_t u = 0; u < U; ++u) {
+                            const uint32_t e = (uint32_t)__shfl((int)excl, (int)(lo[u] + st), 64);
+                            if (e <= qv[u]) lo[u] += st;
                         }
-                        bool sat;
-                        const int64_t d = q_fix_finite(p.lr * (td_o * ev), sat);
-                        if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
-                        if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
-                        const double en = ev * p.gl;
-                        if (in_lds) pc.TRE[col] = en;
-                        else p.trace[(uint64_t)j * Ls + lane_o] = en;
+                    }
+                    uint32_t jv[U], utv[U], wv[U], colv[U];
+                    uint64_t lanev[U];
+                    double tdv[U], evv[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        jv[u] = qv[u] - (uint32_t)__shfl((int)excl, (int)lo[u], 64);
+                        tdv[u] = __shfl(td, (int)lo[u], 64);
+                        utv[u] = P == 2 ? (uint32_t)__shfl((int)ut, (int)lo[u], 64) : 0u;
+                        lanev[u] = lane - lid + lo[u];        // lanes of a wave are consecutive
+                        colv[u] = jv[u] * nthr + wbase + lo[u];
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        wv[u] = 0; evv[u] = 0.0;
+                        if (qv[u] < T) {
+                            const bool in_lds = jv[u] < pc.cap;
+                            wv[u] = in_lds ? (uint32_t)pc.TRI[colv[u]] : (uint32_t)p.tlist[(uint64_t)jv[u] * Ls + lanev[u]];
+                            evv[u] = in_lds ? pc.TRE[colv[u]] : p.trace[(uint64_t)jv[u] * Ls + lanev[u]];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        if (qv[u] < T) {
+                            const uint32_t w = wv[u], j = jv[u], col = colv[u], ut_o = utv[u];
+                            const double ev = evv[u], td_o = tdv[u];
+                            const bool in_lds = j < pc.cap;
+                            const uint32_t id = w & 0x7fffu;
+                            const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
+                            if (w & 0x8000u) {                    // the state's row: n += 1
+                                ++trace_states;
+                                const uint32_t rid = ut_o * SL + lrow(o);
+                                if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                                else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+                            }
+                            bool sat;
+                            const int64_t d = q_fix_finite(p.lr * (td_o * ev), sat);
+                            if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
+                            if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
+                            const double en = ev * p.gl;
+                            if (in_lds) pc.TRE[col] = en;
+                            else p.trace[(uint64_t)j * Ls + lanev[u]] = en;
+                        }
                     }
                 }
                 if (train && term) pair_clear(p, pc, lane, tcnt);

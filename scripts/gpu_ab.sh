@@ -8,9 +8,9 @@ if [ -n "$TESTS" ]; then
   RLAMD_LIB=$PWD/$V timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_ab.log 2>&1
   rc=$?; echo "variant pytest rc=$rc"; tail -2 gpurun_out/pytest_ab.log; [ $rc -eq 0 ] || { grep -m5 -B5 "Error\|assert" gpurun_out/pytest_ab.log | head -40; exit $rc; }
 fi
-for i in 1 2 3; do
-  for w in base var; do
-    if [ $w = var ]; then L=$PWD/$V; else L=$PWD/rl-rust_amd/lib/librlamd.so; fi
+for i in $(seq ${REPS:-3}); do
+  for w in base ${VARS:-${VAR:-1}}; do
+    if [ $w = base ]; then L=$PWD/rl-rust_amd/lib/librlamd.so; else L=$PWD/rl-rust_amd/exp/librlamd_$w.so; fi
     RLAMD_LIB=$L timeout -k 10 200 python -u bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab_$w.log 2>&1 || { tail -5 gpurun_out/ab_$w.log; exit 1; }
     python -c "
 import json
