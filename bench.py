@@ -100,7 +100,7 @@ def counters_for(args):
     if not c:
         return None
     want = {"env": args.env, "algo": args.algo, "lanes": args.lanes, "group": args.group, "sync": args.sync,
-            "slippery": args.slippery}
+            "slippery": args.slippery, "reset_step": args.reset_step}
     return c if all(c.get(k) == v for k, v in want.items()) else None
 
 

@@ -46,7 +46,7 @@ def main():
     tab = json.load(open(path)) if os.path.exists(path) else {}
     hb = s.get("hbm_bytes_per_launch", {})
     tab[key] = {"env": pr["env"], "algo": pr["algo"], "lanes": pr["lanes"], "group": pr["group"],
-                "sync": 64, "slippery": a.slippery,
+                "sync": 64, "slippery": a.slippery, "reset_step": pr.get("reset_step", 0),
                 "hbm_bytes_per_launch": hb.get("total"),
                 "valu_busy_frac": s.get("valu_busy_frac"),
                 "lds_active_frac": s.get("lds_active_frac"),
