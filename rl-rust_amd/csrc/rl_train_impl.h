@@ -476,7 +476,7 @@ __device__ __forceinline__ void fold_flags(uint8_t *QF8, uint32_t idx) {
 // HITS: count clamp hits / delta saturations (off only where the host proved both 0:
 // KParams::hits_zero)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1,
-          bool HITS = true, bool PACK = false>
+          bool HITS = true, bool PACK = false, int RS = -1>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -748,8 +748,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         // that needs a reset does env.reset() + get_action against the step
         // snapshot and then steps in the same synchronous step
         bool fused = false;
-        if constexpr (!UCB) {
-            if (p.reset_step) {
+        if constexpr (!UCB && RS != 0) {   // RS: the schedule as a compile-time constant (-1: KParams)
+            if (RS == 1 || p.reset_step) {
                 if (doR) {
                     const uint32_t s0 = E::reset(L.z, L.rng, tabs);
                     L.ready = true;
@@ -1141,17 +1141,32 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // the host proved both counts 0 (KParams::hits_zero), else k_train_shared.
 template <int SEL, int ALGO>
 constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA; }
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, bool PACK>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, bool PACK, int RS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>(), PACK>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>(), PACK, RS>(p);
 }
+// the reset-and-step schedule is compiled into the 8-wave kernels only where it
+// is the measured better schedule (Blackjack, eps-greedy); elsewhere it runs on
+// k_train_shared, and the 8-wave kernels carry no trace of it
+template <int ENV, int SEL>
+constexpr bool o8_has_reset_step() { return ENV == RL_ENV_BLACKJACK && SEL == RL_SEL_EPS_GREEDY; }
 // the 8-wave kernel for (SLIP, SWEEP), packed contributions when the host proved them exact
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int RS>
+const void *o8_kernel_rs(const KParams &p) {
+    if constexpr (!o8_counts_hits<SEL, ALGO>()) {
+        if (p.pack_ok) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, true, RS>;
+    }
+    return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, false, RS>;
+}
+// nullptr: no 8-wave kernel for this schedule (the caller takes k_train_shared)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
 const void *o8_kernel(const KParams &p) {
-    if constexpr (!o8_counts_hits<SEL, ALGO>()) {
-        if (p.pack_ok) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, true>;
+    if constexpr (o8_has_reset_step<ENV, SEL>()) {
+        if (p.reset_step) return o8_kernel_rs<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1>(p);
+    } else {
+        if (p.reset_step && SEL == RL_SEL_EPS_GREEDY) return nullptr;
     }
-    return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, false>;
+    return o8_kernel_rs<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 0>(p);
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
@@ -1416,8 +1431,9 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
                        : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>(p);
             }
           } else {
-            k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+            k = nullptr;
           }
+          if (!k) k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         } else {
             k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         }
