@@ -179,6 +179,9 @@ def cpu_baseline(args):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # RLAMD_FORCE_COMM=1 (tests): take the multi-GPU code path (gloo control plane,
+    # librlamd's RCCL communicator attached) even with one rank
+    dist_on = world > 1 or os.environ.get("RLAMD_FORCE_COMM") == "1"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch  # loaded before librlamd so both share one HIP runtime
@@ -190,7 +193,7 @@ def main():
     collective = os.environ.get("RLAMD_COLLECTIVE", "rccl")
     dev = local_rank if collective == "rccl" else local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if dist_on:
         dist.init_process_group(os.environ.get("RLAMD_DIST_BACKEND", "gloo"))
     import rlamd
 
@@ -207,12 +210,12 @@ def main():
     torch.cuda.set_stream(stream)
     agent.set_stream(stream.cuda_stream)
     delta, comm = None, None
-    if world > 1 and collective == "rccl":
+    if dist_on and collective == "rccl":
         box = [rlamd.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         comm = rlamd.Comm(rank, world, box[0], dev)
         agent.set_comm(comm)                # every merge: RCCL int64 sum of the delta, then apply
-    elif world > 1:
+    elif dist_on:
         delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
 
@@ -227,7 +230,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     st0 = agent.stats()
@@ -239,7 +242,7 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -249,7 +252,7 @@ def main():
     # RESET steps (env.reset + first get_action) are not env steps
     steps_done = st1["train_steps"] - st0["train_steps"]
     assert 0 < steps_done <= args.steps * args.sync * args.lanes, steps_done
-    if world > 1:                           # control plane (gloo, host tensors)
+    if dist_on:                           # control plane (gloo, host tensors)
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
@@ -284,7 +287,7 @@ def main():
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
                    "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"
-                                  else "torch all_reduce (rehearsal)") if world > 1 else "none",
+                                  else "torch all_reduce (rehearsal)") if dist_on else "none",
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"]},
         # `frac` prices SURVEY §8(d)'s algorithmic bytes (32 B/env-step) against HBM
         # peak; the fused kernel keeps lane records in registers for K steps, so the
@@ -316,7 +319,7 @@ def main():
     agent.close()
     if comm is not None:
         comm.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -71,3 +71,22 @@ def test_bench_two_ranks_prints_one_line():
     # whole-job value: both ranks' env-steps over the max-over-ranks wall time
     assert d["value"] > 0 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["env_steps_per_launch"] <= 64 * (1 << 16)
+
+
+@pytest.mark.gpu
+def test_bench_rccl_path_one_rank():
+    """bench.py's multi-GPU code path with librlamd's own RCCL merge (the one the
+    driver's N = 2/4/8 runs take: gloo bootstrap of the RCCL id, rl_comm_init,
+    rl_agent_set_comm, the all-reduce inside every launch), run with one rank —
+    the box has one GPU and RCCL refuses two ranks on one device."""
+    env = dict(os.environ, RLAMD_FORCE_COMM="1", MASTER_ADDR="127.0.0.1")
+    env.pop("RLAMD_COLLECTIVE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--steps", "3",
+           "--warmup", "1", "--lanes", str(1 << 16), "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["config"]["collective"].startswith("rccl") and d["value"] > 0
