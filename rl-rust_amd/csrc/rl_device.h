@@ -391,6 +391,14 @@ constexpr int64_t Q_RAW_MAX = (int64_t)1 << 51;
 // finite delta -> raw: d*2^40 clamped to +-2^51 then rounded half-to-even; the
 // 1.5*2^52 magic add performs rint and the f64->int64 conversion at once.
 // `sat` is set when |d| exceeds the range (rl_stats::delta_saturations).
+// rint(x) as int64 for |x| < 2^51 (the 1.5*2^52 magic add rounds half-to-even)
+__device__ __forceinline__ int64_t rint_i64_small(double x) {
+    const double y = x + 0x1.8p52;
+    return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
+}
+// q_fix_finite without the range clamp: only where the host proved |d| * 2^40 < 2^51
+// (KParams::hits_zero), so the clamp could not engage
+__device__ __forceinline__ int64_t q_fix_inrange(double d) { return rint_i64_small(d * 0x1p40); }
 __device__ __forceinline__ int64_t q_fix_finite(double d, bool &sat) {
     double x = d * 0x1p40;
     sat = __builtin_fabs(x) > 0x1p51;
@@ -792,8 +800,11 @@ __device__ __forceinline__ double future_q(const double (&q2)[A], uint32_t a2, c
     }
 }
 // decay_epsilon (uniform_epsilon_greed.rs:42-49) with the bins' closure
+// new = eps * dm - ds with (dm, ds) = (f, 0) for a*f or (1, d) for a-d: both products
+// and differences are exact where the two-branch form is (x*1 = x, x-0 = x), so
+// the result is bit-identical without a per-lane select on the decay kind
 __device__ __forceinline__ double decay_eps(const KParams &p, double eps) {
-    const double nw = p.decay_kind == RL_DECAY_MUL ? eps * p.eps_decay : eps - p.eps_decay;
+    const double nw = eps * p.eps_dm - p.eps_ds;
     return p.eps_final > nw ? eps : nw;
 }
 

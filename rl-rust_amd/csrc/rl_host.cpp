@@ -608,6 +608,11 @@ double delta_bound(const rl_agent *a) {
     const double R = env_reward_bound(c.env.kind);
     const double mb = std::max(a->q_abs0, R / (1.0 - g));
     if (!(mb <= 2000.0)) return inf;
+    // the kernels that rely on this bound also convert episode rewards (at most
+    // max_steps + 1 steps of |r| <= R; Blackjack: one +-1) to 2^-16 fixed point
+    // with a rint valid below 2^51
+    const double ep_len = c.env.kind == RL_ENV_BLACKJACK ? 1.0 : (double)c.env.max_steps + 1.0;
+    if (!(ep_len * R * 65536.0 < 0x1p50)) return inf;
     return lr * emax * (R + (1.0 + g) * mb);
 }
 bool hits_proven_zero(const rl_agent *a) { return delta_bound(a) < 2000.0; }
@@ -627,6 +632,8 @@ void agent_sync_params(rl_agent *a) {
     p.eps_final = a->cfg.eps_final;
     p.ucb_c = a->cfg.ucb_c;
     p.decay_kind = a->cfg.decay_kind;
+    p.eps_dm = a->cfg.decay_kind == RL_DECAY_MUL ? a->cfg.eps_decay : 1.0;
+    p.eps_ds = a->cfg.decay_kind == RL_DECAY_MUL ? 0.0 : a->cfg.eps_decay;
     p.algo = a->cfg.algo;
     p.hits_zero = hits_proven_zero(a) ? 1 : 0;
     p.pack_ok = p.hits_zero && pack_proven(a) ? 1 : 0;

@@ -90,6 +90,7 @@ struct KParams {
     double trunc_reward;
     // hyper-parameters
     double lr, gamma, gl, eps_decay, eps_final, ucb_c;
+    double eps_dm, eps_ds;     // decay as eps * dm - ds (rl_device.h decay_eps)
     int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
     // the host proved that no shared-mode Q entry can reach the +-2048 clamp and no
     // TD delta can saturate for these hyper-parameters (rl_host.cpp hits_proven_zero):

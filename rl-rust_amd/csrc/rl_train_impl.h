@@ -695,7 +695,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
         bool hit = false;
         if constexpr (HITS) Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
-        else Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc));
+        else Q[idx] = Q[idx] + (unsigned long long)mean_delta_rcp(sum, rc);   // proven in range: no clamp
         SUM[idx] = 0ull;
         if constexpr (!PACKC) CNT16[idx] = 0;
         if constexpr (SPEC) fold_flags(QF8, idx);
@@ -888,7 +888,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 uint32_t fl = 0;
                 int64_t dq;
                 if constexpr (SPEC) dq = q_fix(p.lr * td, fl, sat);
-                else dq = q_fix_finite(p.lr * td, sat);
+                else if constexpr (HITS) dq = q_fix_finite(p.lr * td, sat);
+                else dq = q_fix_inrange(p.lr * td);
 #if RLAMD_EXP & 2   // timing experiment: no LDS atomics (results differ)
                 owner = dq == 12345;
 #else
@@ -1053,7 +1054,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
             if (INSTR && p.rec) write_record(p, k, lane, fused ? 3u : 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
-            if (tr) atomicAdd(RSUM, (unsigned long long)(int64_t)__builtin_rint(L.epi_reward * 65536.0));
+            // !HITS: the host also proved |episode reward| * 2^16 < 2^51 (delta_bound), so
+            // rint is the magic add
+            if (tr) atomicAdd(RSUM, (unsigned long long)(HITS ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
+                                                               : rint_i64_small(L.epi_reward * 65536.0)));
             if (INSTR && p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         } else if (doR) {
             L.s = s2;
