@@ -272,7 +272,10 @@ def main():
     achieved = bytes_per_launch / avg_kern_s
     pmc = counters_for(args)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    issue = pmc.get("valu_busy_frac") if pmc else None
+    # VALU issue occupancy: ROCm's VALUBusy (SQ_ACTIVE_INST_VALU, 4 cycles per wave64
+    # VALU instruction per SIMD).  Cross-check: SQ_INSTS_VALU x 4 cycles matches the
+    # kernel's cycles on cfg 2 / 5, i.e. these kernels are VALU-issue bound
+    issue = (pmc.get("valu_busy_rocm") or pmc.get("valu_busy_frac")) if pmc else None
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
@@ -300,6 +303,7 @@ def main():
                      "traffic": traffic,
                      "traffic_frac": (traffic / avg_kern_s / HBM_PEAK) if traffic else None,
                      "issue_frac": issue,
+                     "issue_basis": "VALU busy = SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles) (ROCm VALUBusy)",
                      "counters": pmc.get("source") if pmc else None,
                      "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
                      "kernel_launches": n_kern,

@@ -638,7 +638,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // UCB counter increments are applied by the caller after a barrier.
     auto select = [&](uint32_t s, const int64_t (&ra)[A], const int64_t (&rb)[A]) -> uint32_t {
         if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
-            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
+            // one compare decides both the draw (skipped when eps == 0) and the branch
+            bool explore = L.eps != 0.0;
+            if (explore) explore = uniform01(L.rng) < L.eps;
+            if (explore) return uniform_action<A>(L.rng);
             int64_t v[A];                           // argmax of predict() on exact raw sums
 #pragma unroll
             for (int i = 0; i < A; ++i) v[i] = P == 2 ? ra[i] + rb[i] : ra[i];
@@ -1050,7 +1053,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if (doS) {
             if (train) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
-                if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
+                if constexpr (!UCB) {                      // decay_epsilon: one select per lane
+                    const double nw = L.eps * p.eps_dm - p.eps_ds;
+                    L.eps = (term && !(p.eps_final > nw)) ? nw : L.eps;
+                }
             }
             if (INSTR && p.rec) write_record(p, k, lane, fused ? 3u : 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
