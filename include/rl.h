@@ -131,7 +131,8 @@ typedef struct rl_agent_config {
  *   kind 3 RESET + STEP (rl_agent_set_reset_step): s = Env::reset(), a =
  *                 get_action(s), then kind 2 from (s, a)
  *   kind 0: lane idle (finished its train()/evaluate() call)
- * For Blackjack s/s2 are dense indices (see rl_obs_to_reference). */
+ * For Blackjack s/s2 are dense indices (p_score*32 + d_score)*2 + p_ace (S = 2048;
+ * see rl_obs_to_reference). */
 typedef struct rl_step_record {
     uint32_t s, s2;
     uint8_t a, a2, term, mode;

@@ -633,7 +633,7 @@ static int build_env(envdef *E, const rlo_config *c) {
     case RLO_ENV_FROZEN_LAKE_EDITED: build_frozen_lake_edited(E, c->map8x8, c->slippery); return 0;
     case RLO_ENV_CLIFF_WALKING: build_cliff_walking(E); return 0;
     case RLO_ENV_TAXI: build_taxi(E); return 0;
-    case RLO_ENV_BLACKJACK: E->S = 32 * 27 * 2; E->A = 2; return 0;
+    case RLO_ENV_BLACKJACK: E->S = 32 * 32 * 2; E->A = 2; return 0;
     }
     return -1;
 }
@@ -664,7 +664,7 @@ int rlo_env_start(const rlo_config *c, double *start) {
 /* blackjack helpers: src/env/blackjack.rs:47-83 */
 static inline uint32_t bj_score(uint32_t sum, uint32_t ace) { return (ace && sum + 10 <= 21) ? sum + 10 : sum; }
 /* dense obs index: p_score <= 31, d_score <= 26 (dealer stops at >= 17) */
-static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 27 + d) * 2 + (ace ? 1 : 0); }
+static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 32 + d) * 2 + (ace ? 1 : 0); }
 static void bj_initialize_hands(envstate *st, rlo_rng *r) {       /* :47-56 */
     uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
     st->p_sum = p0 + p1; st->d_sum = d0 + d1; st->d0 = d0;
@@ -886,7 +886,7 @@ static void net_features(const envdef *E, const netdef *n, int input, double *fe
             x[4] = (double)row;
             x[5] = (double)col;
         } else if (E->kind == RLO_ENV_BLACKJACK) {
-            x[0] = (double)rlo_blackjack_obs_id(s / 54u, (s >> 1) % 27u, s & 1u);
+            x[0] = (double)rlo_blackjack_obs_id(s >> 6, (s >> 1) & 31u, s & 1u);
         } else {
             x[0] = (double)s;
         }

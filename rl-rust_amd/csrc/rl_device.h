@@ -681,7 +681,7 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         return (ace && sum + 10u <= 21u) ? sum + 10u : sum;      // :58-74
     }
     __device__ static __forceinline__ uint32_t obs(uint32_t p, uint32_t d, uint32_t ace) {
-        return (p * 27u + d) * 2u + ace;
+        return ((p << 5) + d) * 2u + ace;   // dense index (p*32 + d)*2 + ace: shifts to decode
     }
     __device__ static __forceinline__ uint32_t deal(Rng &r) {    // initialize_hands :47-56
         // four words drawn back to back: when none falls in the rejection zone

@@ -239,7 +239,7 @@ int build_env(const rl_env_config &c, EnvHost &e) {
         for (uint32_t i = 0; i < 500u * 6u; ++i)
             if (taxi_word(i / 6u, i % 6u) != e.trans[i]) return fail(RL_E_STATE, "taxi_word differs from the table");
     } else if (c.kind == RL_ENV_BLACKJACK) {
-        e.S = 32 * 27 * 2;   // dense (p_score <= 31, d_score <= 26, p_ace)
+        e.S = 32 * 32 * 2;   // dense (p_score <= 31, d_score <= 26 in 5 bits, p_ace): (p*32 + d)*2 + ace
         e.A = 2;
     } else {
         return fail(RL_E_ARG, "unknown env kind");
@@ -524,7 +524,7 @@ void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f) {
     for (uint32_t t = 0; t < a->P; ++t) {
         bool first = true;
         for (uint32_t s = 0; s < a->S; ++s) {
-            const uint32_t pl = s / 54u, d = (s >> 1) % 27u;
+            const uint32_t pl = s >> 6, d = (s >> 1) & 31u;
             if (pl <= 21u && d <= 10u) continue;
             for (uint32_t b = 0; b < a->A; ++b) {
                 const size_t i = t * SA + (size_t)s * a->A + b;
@@ -782,7 +782,7 @@ uint64_t rl_blackjack_obs_id(uint32_t p, uint32_t d, uint32_t ace) {
     return h;
 }
 uint64_t rl_obs_to_reference(int32_t env_kind, uint32_t s) {
-    if (env_kind == RL_ENV_BLACKJACK) return rl_blackjack_obs_id(s / 54u, (s >> 1) % 27u, s & 1u);
+    if (env_kind == RL_ENV_BLACKJACK) return rl_blackjack_obs_id(s >> 6, (s >> 1) & 31u, s & 1u);
     return s;
 }
 

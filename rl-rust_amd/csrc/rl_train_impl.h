@@ -28,23 +28,23 @@ __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15
 // Blackjack's LDS rows (shared mode, eps-greedy): the learner group's Q copy holds
 // only the states an update can write — non-terminal observations, p <= 21 and
 // dealer card d <= 10 (blackjack.rs:121-162: every other observation ends the
-// episode) — as (p*11 + d)*2 + ace, 484 of the 1728 dense rows.  Terminal rows
+// episode) — as (p*11 + d)*2 + ace, 484 of the 2048 dense rows.  Terminal rows
 // are only read (TD target / selection at s'), never written, so they are read
 // from Q_base in HBM (L2-resident).  UCB writes counters at terminal s' too, so
 // UCB keeps the dense rows.
 constexpr uint32_t BJ_LDS_STATES = 22u * 11u * 2u;
 __host__ __device__ inline bool bj_compact(int env, int ucb) { return env == RL_ENV_BLACKJACK && !ucb; }
 __host__ __device__ inline bool bj_nonterminal(uint32_t s) {
-    const uint32_t p = s / 54u, d = (s >> 1) % 27u;
+    const uint32_t p = s >> 6, d = (s >> 1) & 31u;
     return p <= 21u && d <= 10u;
 }
 __host__ __device__ inline uint32_t bj_row(uint32_t s) {          // dense obs -> LDS row
-    const uint32_t p = s / 54u, r = s - p * 54u;
+    const uint32_t p = s >> 6, r = s & 63u;
     return (p * 11u + (r >> 1)) * 2u + (r & 1u);
 }
 __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> dense obs
     const uint32_t pd = row >> 1, p = pd / 11u, d = pd - p * 11u;
-    return (p * 27u + d) * 2u + (row & 1u);
+    return ((p << 5) + d) * 2u + (row & 1u);
 }
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40)

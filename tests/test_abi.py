@@ -66,7 +66,7 @@ def test_env_dims(rl):
     assert rl.env_dims(rl.default_params(env="frozen_lake", map8x8=1)) == (64, 4)
     assert rl.env_dims(rl.default_params(env="cliff_walking")) == (48, 4)
     assert rl.env_dims(rl.default_params(env="taxi")) == (500, 6)
-    assert rl.env_dims(rl.default_params(env="blackjack")) == (32 * 27 * 2, 2)
+    assert rl.env_dims(rl.default_params(env="blackjack")) == (32 * 32 * 2, 2)
 
 
 def test_blackjack_ids(rl, oracle):
@@ -75,7 +75,7 @@ def test_blackjack_ids(rl, oracle):
         for d in range(27):
             for a in range(2):
                 assert L.rl_blackjack_obs_id(p, d, a) == O.rlo_blackjack_obs_id(p, d, a)
-                s = (p * 27 + d) * 2 + a
+                s = (p * 32 + d) * 2 + a
                 assert L.rl_obs_to_reference(3, s) == O.rlo_blackjack_obs_id(p, d, a)
     assert L.rl_obs_to_reference(0, 17) == 17
 

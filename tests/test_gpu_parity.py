@@ -110,12 +110,12 @@ def test_env_trait_streams(rl, oracle, env, map8, slip):
     for lane in range(n):
         s0, s2, r, t, k = oracle.env_walk(p, acts[:steps, lane], lane=lane)
         ref0 = s0 if env != "blackjack" else oracle.lib().rlo_blackjack_obs_id(
-            s0 // 54, (s0 >> 1) % 27, s0 & 1)
+            s0 >> 6, (s0 >> 1) & 31, s0 & 1)
         assert obs0[lane] == ref0
         m = min(k, steps)
         for j in range(m):
             ref = s2[j] if env != "blackjack" else oracle.lib().rlo_blackjack_obs_id(
-                s2[j] // 54, (s2[j] >> 1) % 27, s2[j] & 1)
+                s2[j] >> 6, (s2[j] >> 1) & 31, s2[j] & 1)
             assert dev_s[j][lane] == ref and dev_r[j][lane] == r[j] and dev_t[j][lane] == t[j]
 
 
@@ -451,7 +451,7 @@ def test_blackjack_terminal_rows_after_set_q(rl, oracle, terminal):
     rng = np.random.default_rng(11)
     q = rng.uniform(-1.0, 1.0, (P, S, A))
     s = np.arange(S)
-    term = ~((s // 54 <= 21) & ((s >> 1) % 27 <= 10))
+    term = ~((s >> 6 <= 21) & ((s >> 1) & 31 <= 10))
     if terminal == "uniform":
         q[0][term] = 0.375
         q[1][term] = -0.125

@@ -95,7 +95,7 @@ def test_set_q_fixed_point_and_blackjack_terminal_rows(oracle):
     qq = b.q()
     assert np.isnan(qq[0, 5, 1]) and qq[1, 7, 0] == np.inf
     s = np.arange(S)
-    term = ~((s // 54 <= 21) & ((s >> 1) % 27 <= 10))
+    term = ~((s >> 6 <= 21) & ((s >> 1) & 31 <= 10))
     before = raw[:, term, :].copy()
     b.run(6)
     assert np.array_equal(b.q_raw()[:, term, :], before)
