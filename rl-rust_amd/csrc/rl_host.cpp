@@ -573,15 +573,21 @@ double env_reward_bound(int kind) {
 }
 
 // Can a shared-mode entry reach the |Q| <= 2048 clamp, or a TD delta saturate at
-// +-2^51 raw?  Not when the bootstrap F is a sub-convex combination of Q values —
+// +-2^51 raw?  Provable only for the one-step agent on a single table: the
+// double policy writes one table with a TD error taken on the other
+// (double_tabular_policy.rs:31-67: Q_u += lr*(r + gamma*F - Q_v)), and the
+// eligibility traces move every visited entry by the CURRENT pair's error
+// (elegibility_traces_agent.rs:82-96) — neither update contracts the entry it
+// writes (the double policy's A - B grows by (1 + lr) per update pair; cfg 5 clamps
+// at bench length), so both are counted, never assumed.  For the one-step
+// tabular agent, not when the bootstrap F is a sub-convex combination of Q values —
 // SARSA's pick, Q-learning's max, expected SARSA over eps-greedy's probabilities
 // (eps/A each and 1-eps at the argmax: non-negative for eps in [0,1], summing to
 // 1-eps/A; src/agent.rs:19-45, uniform_epsilon_greed.rs:72-76).  Then one update
-// Q' = (1-w)Q + w(r + gamma*F), w = lr*E in [0,1] (E = the trace, <= 1/(1-gamma*
-// lambda) for the accumulating trace, 1 for one-step), keeps |Q'| <= max(M,
-// R/(1-gamma)) when |Q|, |F| <= M; a step's mean of such values and the merge's
-// mean over groups keep the bound, so by induction every entry stays within
-// Mb = max(|Q_0|, R/(1-gamma)), and every delta within lr*E*(R + (1+gamma)Mb).
+// Q' = (1-lr)Q + lr(r + gamma*F) with lr in [0,1] keeps |Q'| <= max(M, R/(1-gamma))
+// when |Q|, |F| <= M; a step's mean of such values and the merge's mean over groups
+// keep the bound, so by induction every entry stays within Mb = max(|Q_0|,
+// R/(1-gamma)), and every delta within lr*(R + (1+gamma)Mb).
 // UCB + expected SARSA weighs by u_i / sum(u) (upper_confidence_bound.rs:48-63):
 // no bound, its kernels always count.
 // Returns the proven bound on |lr * E * td| (+inf when nothing is proven); the
@@ -590,15 +596,11 @@ double delta_bound(const rl_agent *a) {
     const double inf = std::numeric_limits<double>::infinity();
     const rl_agent_config &c = a->cfg;
     if (a->priv || a->neural) return inf;
+    if (c.agent != RL_AGENT_ONE_STEP || c.policy != RL_POLICY_TABULAR) return inf;
     if (c.selector == RL_SEL_UCB && c.algo == RL_ALGO_EXPECTED_SARSA) return inf;
     const double lr = c.lr, g = c.gamma;
     if (!(lr >= 0.0 && g >= 0.0 && g < 1.0 && std::isfinite(a->q_abs0))) return inf;
-    double emax = 1.0;
-    if (c.agent == RL_AGENT_TRACES) {
-        const double gl = g * c.lambda;
-        if (!(gl >= 0.0 && gl < 1.0)) return inf;
-        emax = 1.0 / (1.0 - gl);
-    }
+    const double emax = 1.0;   // one-step: the written entry's own error, weight lr
     if (!(lr * emax <= 1.0)) return inf;
     if (c.selector == RL_SEL_EPS_GREEDY && c.algo == RL_ALGO_EXPECTED_SARSA) {
         // eps stays in [eps_final, eps0] (or decays toward 0 by a factor in [0,1])

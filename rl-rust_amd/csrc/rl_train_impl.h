@@ -1151,9 +1151,11 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // the host proved both counts 0 (KParams::hits_zero), else k_train_shared.
 template <int SEL, int ALGO>
 constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA; }
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, bool PACK, int RS>
+// MODE 0: counts clamp hits / saturations (and clamps); 1: the host proved the
+// range (no counting, no clamps); 2: as 1, with packed (sum, count) contributions
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, o8_counts_hits<SEL, ALGO>(), PACK, RS>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, MODE == 0, MODE == 2, RS>(p);
 }
 // the reset-and-step schedule is compiled into the 8-wave kernels only where it
 // is the measured better schedule (Blackjack, eps-greedy); elsewhere it runs on
@@ -1161,12 +1163,22 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
 template <int ENV, int SEL>
 constexpr bool o8_has_reset_step() { return ENV == RL_ENV_BLACKJACK && SEL == RL_SEL_EPS_GREEDY; }
 // the 8-wave kernel for (SLIP, SWEEP), packed contributions when the host proved them exact
+// nullptr: no 8-wave kernel for this case (unproven range outside Blackjack: the
+// caller takes k_train_shared, which counts)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int RS>
 const void *o8_kernel_rs(const KParams &p) {
-    if constexpr (!o8_counts_hits<SEL, ALGO>()) {
-        if (p.pack_ok) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, true, RS>;
+    if constexpr (o8_counts_hits<SEL, ALGO>()) {
+        return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 0, RS>;
+    } else {
+        if (p.hits_zero)
+            return p.pack_ok ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 2, RS>
+                             : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1, RS>;
+        // Blackjack double Q (cfg 5) is not range-provable (the double policy's update
+        // is not a contraction of the written table), so its 8-wave kernel counts
+        if constexpr (ENV == RL_ENV_BLACKJACK)
+            return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 0, RS>;
+        return nullptr;
     }
-    return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, false, RS>;
 }
 // nullptr: no 8-wave kernel for this schedule (the caller takes k_train_shared)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
@@ -1426,8 +1438,7 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
         k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, true>;
     } else {
         if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) {
-          if (o8_counts_hits<SEL, ALGO>() || p.hits_zero) {
-            // the map's slippery flag as a compile-time constant (FrozenLake only)
+          {
             // the map's slippery flag (FrozenLake) and the settle form (every entry
             // owned by one thread when P*S*A <= block size) as compile-time constants
             const bool sw = p.P * p.S * p.A <= block.x;
@@ -1440,8 +1451,6 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
                 k = sw ? o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>(p)
                        : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>(p);
             }
-          } else {
-            k = nullptr;
           }
           if (!k) k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         } else {

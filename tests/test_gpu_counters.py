@@ -142,3 +142,22 @@ def test_train_then_run_keeps_training(rl, oracle, G):
         _assert_q_equal(dev.q(), ref.q())
     else:
         assert np.array_equal(dev.q_raw(), ref.q_raw())
+
+
+@pytest.mark.parametrize("reset_step", [False, True], ids=["one-action", "reset-and-step"])
+def test_double_policy_clamps_are_counted_and_exact(rl, oracle, reset_step):
+    """The double policy writes one table with the TD error of the other
+    (double_tabular_policy.rs:31-67), so A - B grows by (1 + lr) per update pair and
+    long runs reach the +-2048 fixed-point clamp (cfg 5 does at bench length): no
+    range proof applies, the 8-wave kernel counts and clamps, bit-exact vs the oracle."""
+    p = rl.default_params(env="blackjack", policy="double", algo="qlearning", n_lanes=4096, group_size=512,
+                          sync_every=64)
+    dev, ref = rl.Agent(p), oracle.Batch(p)
+    dev.set_reset_step(reset_step)
+    ref.set_reset_step(reset_step)
+    dev.run(40)
+    ref.run(40)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    st, rs = dev.stats(), ref.stats()
+    assert st["q_clamp_hits"] == int(rs[8]) and st["q_clamp_hits"] > 0, (st, rs[8])
+    _assert_stats_equal(dev, ref)
