@@ -49,6 +49,8 @@ def main():
                 "sync": 64, "slippery": a.slippery, "reset_step": pr.get("reset_step", 0),
                 "hbm_bytes_per_launch": hb.get("total"),
                 "valu_busy_frac": s.get("valu_busy_frac"),
+                "valu_pipe_frac": s.get("valu_pipe_frac"),
+                "valu_busy_rocm": s.get("valu_busy_rocm"),
                 "lds_active_frac": s.get("lds_active_frac"),
                 "lds_bank_conflict_frac": (s["pmc_mean_per_launch"].get("SQ_LDS_BANK_CONFLICT", 0.0) /
                                            s["pmc_mean_per_launch"]["SQ_LDS_IDX_ACTIVE"])
@@ -56,8 +58,9 @@ def main():
                 "wave_cycle_split": s.get("wave_cycle_split"),
                 "kernel_avg_ns": s.get("kernel_avg_ns"),
                 "source": f"profiles/{stem}_summary.json: rocprofv3 separate --pmc passes (FETCH_SIZE x2 "
-                          f"gfx950 correction + WRITE_SIZE; SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE/8 x 1024 "
-                          f"SIMDs)), mean per launch of the dominant kernel, HEAD {head}"}
+                          f"gfx950 correction + WRITE_SIZE; VALU pipe occupancy = (2 x SQ_INSTS_VALU + 2 x (FP64 "
+                          f"add/mul/fma + INT64) + 6 x TRANS_F64) cycles / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs)), mean "
+                          f"per launch of the dominant kernel, HEAD {head}"}
     json.dump(tab, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps(tab[key], indent=1))
 
