@@ -81,7 +81,7 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.n = off;
     l.nd = off + align16(SA * 4u);
     off += (shared_q && ucb) ? (ucb == 2 ? align16(SA * 4u) + align16(((SA + 1u) / 2u) * 4u) : align16(SA * 8u)) : 0u;
-    l.t = off; off += (shared_q && ucb) ? 16u : 0u;
+    l.t = off; off += (shared_q && ucb) ? (ucb == 2 ? 32u : 16u) : 0u;   // T[0], T[1] (+ ARR: UCB + ES)
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
     l.rcp = off; off += align16(l.nrcp * 8u);
     l.tr = off; off += (env == RL_ENV_TAXI || env == RL_ENV_BLACKJACK) ? 0u : align16(SA * 4u);
@@ -548,7 +548,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         } else {
             for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = (unsigned long long)p.n_base[i];
         }
-        if (tid == 0) { T[0] = p.t_base[0]; T[1] = 0ull; }
+        if (tid == 0) {
+            T[0] = p.t_base[0]; T[1] = 0ull;
+            if constexpr (SPEC) *(uint32_t *)(T + 2) = 0u;
+        }
     }
     if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
@@ -819,7 +822,23 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[1], (unsigned long long)c);
-            __syncthreads();
+            // one-sided barrier: every wave announces that its increments are in
+            // (ARR counts arrivals over the launch); only a wave with a lane whose
+            // target row is finite reads n + D / T, so only such a wave waits for all
+            // arrivals of this step.  No wave passes the end-of-step barrier before
+            // arriving, so ARR >= (k+1) * waves means exactly that.  In the all-NaN
+            // regime no wave waits.  What the others go on to do meanwhile (SUM/CNT
+            // contributions, pending QF bits) is invisible to the step's readers.
+            uint32_t *ARR = (uint32_t *)(T + 2);
+            __threadfence_block();
+            if ((tid & 63u) == 0) atomicAdd(ARR, 1u);
+            if (__ballot(train_lane && !tgt_nf)) {
+                const uint32_t goal = (k + 1u) * (nthr >> 6);
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ARR, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < goal)
+                    __builtin_amdgcn_s_sleep(1);
+                __threadfence_block();
+            }
             lnt_ok = false;   // this step's probabilities and the next selection use ln(T_{k+1})
         } else if constexpr (UCB) {
             __syncthreads();
