@@ -919,7 +919,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #endif
             }
             if constexpr (HITS) c_sat += (uint32_t)__popcll(__ballot(sat));
+#if !(RLAMD_EXP & 16)   // timing experiment: no contributions barrier (results differ)
             __syncthreads();   // all contributions in, all Q reads done
+#endif
             bool hit = false;
 #if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
             if (sweep) { if (tid < PSA && CNT16[tid] == 77) hit = settle(tid); }
@@ -1067,7 +1069,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (d_own != 0xffffffffu) { NL[d_own] += (uint32_t)D16[d_own]; D16[d_own] = 0; }
             if (tid == 0) { T[0] += T[1]; T[1] = 0ull; }
         }
+#if !(RLAMD_EXP & 8)   // timing experiment: no end-of-step barrier (results differ)
         __syncthreads();   // Q_{t+1} complete before the next step's reads
+#endif
         bool tr = false, ev = false;
         if (doS) {
             if (train) {
@@ -1173,7 +1177,10 @@ constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EX
 // MODE 0: counts clamp hits / saturations (and clamps); 1: the host proved the
 // range (no counting, no clamps); 2: as 1, with packed (sum, count) contributions
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) k_train_shared_o8(KParams p) {
+#ifndef RLAMD_O8_WAVES
+#define RLAMD_O8_WAVES 8   // waves per SIMD the o8 kernels are compiled for (timing experiments: 6)
+#endif
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RLAMD_O8_WAVES, RLAMD_O8_WAVES))) k_train_shared_o8(KParams p) {
     train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, MODE == 0, MODE == 2, RS>(p);
 }
 // the reset-and-step schedule is compiled into the 8-wave kernels only where it
