@@ -44,18 +44,23 @@ __host__ __device__ inline uint32_t taxi_word(uint32_t s, uint32_t a) {
 // The answer is the first k with c_k > u (else state 0, u >= c_300 =
 // 0.9999999999999961).  c_k = k/300 within 1e-13 while the c_k are 1/300 apart,
 // so k is one of floor(u*300) .. floor(u*300)+2: three probes of the HBM cdf
-// instead of a 500-entry LDS table (build_env checks every boundary).
+// instead of a 500-entry LDS table (build_env checks every boundary).  The three
+// loads are independent (issued together: one memory latency, not three) and
+// the first probe whose c_k > u wins, as a scan would find it.
 __host__ __device__ inline uint32_t taxi_start_state(uint32_t k) {   // k = 1..300
     const uint32_t k0 = k - 1u, cell = k0 / 12u, j = k0 - cell * 12u, pass = j / 3u, r3 = j - pass * 3u;
     return cell * 20u + pass * 4u + r3 + (r3 >= pass ? 1u : 0u);
 }
 __host__ __device__ inline uint32_t taxi_start(const double *cdf, double u) {
     const uint32_t g = (uint32_t)(u * 300.0);
-    uint32_t k = g < 1u ? 1u : g;
-    for (int i = 0; i < 3 && k <= 300u; ++i, ++k) {
-        const uint32_t st = taxi_start_state(k);
-        if (cdf[st] > u) return st;
-    }
+    const uint32_t k = g < 1u ? 1u : g;                    // <= 300: u < 1
+    const uint32_t s0 = taxi_start_state(k);
+    const uint32_t s1 = k + 1u <= 300u ? taxi_start_state(k + 1u) : s0;
+    const uint32_t s2 = k + 2u <= 300u ? taxi_start_state(k + 2u) : s0;
+    const double c0 = cdf[s0], c1 = cdf[s1], c2 = cdf[s2];
+    if (c0 > u) return s0;
+    if (k + 1u <= 300u && c1 > u) return s1;
+    if (k + 2u <= 300u && c2 > u) return s2;
     return 0u;
 }
 
