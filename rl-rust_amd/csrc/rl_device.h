@@ -445,6 +445,20 @@ __device__ __forceinline__ uint32_t argmax_i64(const int64_t (&v)[A]) {
         if (v[i] > m) { m = v[i]; r = (uint32_t)i; }
     return r;
 }
+// argmax and max of one row in a single pass (first maximum, strict `>`): the
+// index is argmax_i64's and the value max_i64's
+template <int A>
+__device__ __forceinline__ uint32_t argmax_max_i64(const int64_t (&v)[A], int64_t &m) {
+    m = v[0];
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 1; i < A; ++i) {
+        const bool gt = v[i] > m;
+        m = gt ? v[i] : m;
+        r = gt ? (uint32_t)i : r;
+    }
+    return r;
+}
 template <int A>
 __device__ __forceinline__ int64_t max_i64(const int64_t (&v)[A]) {
     int64_t m = v[0];
@@ -452,11 +466,18 @@ __device__ __forceinline__ int64_t max_i64(const int64_t (&v)[A]) {
     for (int i = 1; i < A; ++i) m = v[i] > m ? v[i] : m;
     return m;
 }
+// x unchanged, but opaque to the optimizer (an empty asm): a select chain over
+// opq(v[j]) cannot be folded back into v[i], which would put v in scratch memory
+template <class T>
+__device__ __forceinline__ T opq(T x) {
+    asm("" : "+v"(x));
+    return x;
+}
 template <int A, class T>
-__device__ __forceinline__ T pick(const T (&v)[A], uint32_t i) {   // v[i] as a select chain
-    T r = v[0];
+__device__ __forceinline__ T pick(const T (&v)[A], uint32_t i) {   // v[i] as a select chain (in registers)
+    T r = opq(v[0]);
 #pragma unroll
-    for (int j = 1; j < A; ++j) r = (i == (uint32_t)j) ? v[j] : r;
+    for (int j = 1; j < A; ++j) r = (i == (uint32_t)j) ? opq(v[j]) : r;
     return r;
 }
 

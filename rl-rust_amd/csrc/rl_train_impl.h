@@ -328,12 +328,24 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // the 8-wave kernel), so off
 #define RLAMD_BJ_ONE_LOOP 0
 #endif
+#ifndef RLAMD_FUSE_MAX
+#define RLAMD_FUSE_MAX 2   // single-table Q-learning: one argmax+max pass per step (0: off,
+                           // 1: fused, 2: fused and pinned before the selection)
+#endif
 #ifndef RLAMD_SWEEP_U
 #define RLAMD_SWEEP_U 4   // pair-trace sweep: rounds of 64 items interleaved per iteration
                           // (cfg 4: 1 / 2 / 4 -> 1.163 / 1.089 / 1.058 ms per launch)
 #endif
 #ifndef RLAMD_COOP_SWEEP
 #define RLAMD_COOP_SWEEP 1   // shared pair traces: wave-cooperative sweep (0: each lane its own list)
+#endif
+#ifndef RLAMD_PAIR_BITS
+#define RLAMD_PAIR_BITS 1   // small tables: visited-pair bitmap in registers (0: scan the list)
+#endif
+#ifndef RLAMD_TRACES_W
+#define RLAMD_TRACES_W 0   // small-table traces at <= 2 groups per CU: a 256-VGPR kernel
+                           // (measured equal on cfg 4 once the bitmap and opq() removed the
+                           // scratch arrays: 0.8875 vs 0.8869 ms, so off)
 #endif
 #ifndef RLAMD_PAIR_TC
 #define RLAMD_PAIR_TC 8   // HBM pair slots per batch of the sweep (loads issued together)
@@ -594,6 +606,35 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * nthr * 2u)),
                        lay.trc_cap, nthr, tid};
     if constexpr (PAIRS) { if (active) pair_cache_load(p, pc, lane, tcnt); }
+    // small tables (S*A <= 256: FrozenLake, CliffWalking): the lane's visited-pair set
+    // as a bitmap in registers, rebuilt from the list at launch start.  A visit then
+    // needs no scan: a new pair is appended, a visited one gets its E += 1 inside the
+    // sweep (the same f64 add, before its use), and "first pair of its state" is the
+    // state's A bits
+    constexpr bool PBITS = PAIRS && RLAMD_COOP_SWEEP && RLAMD_PAIR_BITS &&
+                           (ENV == RL_ENV_CLIFF_WALKING || ENV == RL_ENV_FROZEN_LAKE ||
+                            ENV == RL_ENV_FROZEN_LAKE_EDITED);
+    constexpr int PBW = ENV == RL_ENV_CLIFF_WALKING ? 6 : 8;   // 48*4 / 64*4 pair ids
+    uint32_t pbits[PBW];
+#pragma unroll
+    for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
+    auto pbits_word = [&](uint32_t wi) -> uint32_t {
+        uint32_t w = opq(pbits[0]);
+#pragma unroll
+        for (int i = 1; i < PBW; ++i) w = wi == (uint32_t)i ? opq(pbits[i]) : w;
+        return w;
+    };
+    auto pbits_set = [&](uint32_t id) {
+#pragma unroll
+        for (int i = 0; i < PBW; ++i) pbits[i] |= (id >> 5) == (uint32_t)i ? (1u << (id & 31u)) : 0u;
+    };
+    if constexpr (PBITS) {
+        static_assert(A == 4, "a state's pair bits sit in one bitmap word");
+        if (active)
+            for (uint32_t j = 0; j < tcnt; ++j)
+                pbits_set((j < pc.cap ? (uint32_t)pc.TRI[pc.ix(j)] : (uint32_t)p.tlist[(uint64_t)j * p.L + lane]) &
+                          0x7fffu);
+    }
 
     // the A visible-flag bytes of LDS row s of table tbl, one per action (A <= 6:
     // the row starts at byte A*(tbl*SL + s), at most 2 bytes into its first word,
@@ -639,12 +680,17 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     };
     // Agent::get_action = selector(Policy::predict(s)) against the step snapshot;
     // UCB counter increments are applied by the caller after a barrier.
-    auto select = [&](uint32_t s, const int64_t (&ra)[A], const int64_t (&rb)[A]) -> uint32_t {
+    // single-table Q-learning: the selection's argmax and the TD target's max are
+    // of the same row s2, so both come from one pass (argmax_max_i64) computed for
+    // the whole wave before the selection; `pre` is that argmax (-1: none)
+    constexpr bool FUSE_MAX = RLAMD_FUSE_MAX && !UCB && P == 1 && ALGO == RL_ALGO_QLEARNING;
+    auto select = [&](uint32_t s, const int64_t (&ra)[A], const int64_t (&rb)[A], int32_t pre = -1) -> uint32_t {
         if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
             // one compare decides both the draw (skipped when eps == 0) and the branch
             bool explore = L.eps != 0.0;
             if (explore) explore = uniform01(L.rng) < L.eps;
             if (explore) return uniform_action<A>(L.rng);
+            if constexpr (FUSE_MAX) return (uint32_t)pre;
             int64_t v[A];                           // argmax of predict() on exact raw sums
 #pragma unroll
             for (int i = 0; i < A; ++i) v[i] = P == 2 ? ra[i] + rb[i] : ra[i];
@@ -760,7 +806,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     const uint32_t s0 = E::reset(L.z, L.rng, tabs);
                     L.ready = true;
                     load_rows(s0, ra2, rb2);
-                    L.a = select(s0, ra2, rb2);
+                    L.a = select(s0, ra2, rb2, FUSE_MAX ? (int32_t)argmax_i64<A>(ra2) : -1);
                     L.s = s0;
                     L.need_reset = false;
                     L.epi_reward = 0.0;
@@ -806,10 +852,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
             for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
         }
+        int64_t rmax = 0;                   // FUSE_MAX: utils::max of row s2 (the Q-learning target)
+        int32_t rarg = -1;
+        if constexpr (FUSE_MAX) {
+            rarg = (int32_t)argmax_max_i64<A>(ra2, rmax);
+            // pin both here (empty asm): left alone, the compiler sinks the index into
+            // the exploit branch and the max into the TD branch, redoing the compares
+            if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmax));
+        }
 #if RLAMD_EXP & 4   // timing experiment: greedy selection, no RNG (results differ)
         if (alive) { int64_t v[A]; for (int i = 0; i < A; ++i) v[i] = ra2[i]; a2 = argmax_i64<A>(v); }
 #else
-        if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2);
+        if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2, rarg);
 #endif
         uint32_t d_own = 0xffffffffu;   // SPEC: the D entry this lane settles at step end
         if constexpr (SPEC) {
@@ -859,7 +913,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             for (int i = 0; i < A; ++i) rv[i] = vt ? rb2[i] : ra2[i];
             double fq;
             if constexpr (ALGO == RL_ALGO_QLEARNING && !SPEC) {
-                fq = q_val(max_i64<A>(rv));                // utils::max on exact images
+                fq = q_val(FUSE_MAX ? rmax : max_i64<A>(rv));   // utils::max on exact images
             } else if constexpr (ALGO == RL_ALGO_SARSA && !SPEC) {
                 fq = q_val(pick<A>(rv, a2));
             } else if (SPEC && tgt_nf) {
@@ -936,7 +990,30 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
             // own visited set; slot j of all lanes is one coalesced row.
             if constexpr (PAIRS && RLAMD_COOP_SWEEP) {
-                if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
+                uint32_t hid = 0xffffu;      // PBITS: the visited pair whose E += 1 the sweep applies
+                if constexpr (PBITS) {
+                    if (train) {
+                        const uint32_t id = L.s * (uint32_t)A + L.a;
+                        const uint32_t w = pbits_word(id >> 5);
+                        if ((w >> (id & 31u)) & 1u) {
+                            hid = id;
+                        } else {
+                            const bool first = ((w >> ((L.s * (uint32_t)A) & 31u)) & 0xfu) == 0u;
+                            const uint16_t tag = (uint16_t)(id | (first ? 0x8000u : 0u));
+                            const uint32_t j = tcnt++;
+                            if (j < pc.cap) {
+                                pc.TRI[pc.ix(j)] = tag;
+                                pc.TRE[pc.ix(j)] = 1.0;
+                            } else {
+                                p.tlist[(uint64_t)j * p.L + lane] = tag;
+                                p.trace[(uint64_t)j * p.L + lane] = 1.0;
+                            }
+                            pbits_set(id);
+                        }
+                    }
+                } else {
+                    if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
+                }
                 // wave-cooperative sweep: the (lane, slot) items of the wave's 64
                 // lanes are dealt out 64 at a time, so a wave takes ceil(sum/64)
                 // rounds instead of its longest list (episode lengths are long-tailed)
@@ -968,7 +1045,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             if (e <= qv[u]) lo[u] += st;
                         }
                     }
-                    uint32_t jv[U], utv[U], wv[U], colv[U];
+                    uint32_t jv[U], utv[U], wv[U], colv[U], hidv[U];
                     uint64_t lanev[U];
                     double tdv[U], evv[U];
 #pragma unroll
@@ -976,6 +1053,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         jv[u] = qv[u] - (uint32_t)__shfl((int)excl, (int)lo[u], 64);
                         tdv[u] = __shfl(td, (int)lo[u], 64);
                         utv[u] = P == 2 ? (uint32_t)__shfl((int)ut, (int)lo[u], 64) : 0u;
+                        hidv[u] = PBITS ? (uint32_t)__shfl((int)hid, (int)lo[u], 64) : 0xffffu;
                         lanev[u] = lane - lid + lo[u];        // lanes of a wave are consecutive
                         colv[u] = jv[u] * nthr + wbase + lo[u];
                     }
@@ -992,9 +1070,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     for (uint32_t u = 0; u < U; ++u) {
                         if (qv[u] < T) {
                             const uint32_t w = wv[u], j = jv[u], col = colv[u], ut_o = utv[u];
-                            const double ev = evv[u], td_o = tdv[u];
-                            const bool in_lds = j < pc.cap;
                             const uint32_t id = w & 0x7fffu;
+                            const double ev = (PBITS && id == hidv[u]) ? evv[u] + 1.0 : evv[u], td_o = tdv[u];
+                            const bool in_lds = j < pc.cap;
                             const uint32_t o = id / (uint32_t)A, b = id - o * (uint32_t)A;
                             if (w & 0x8000u) {                    // the state's row: n += 1
                                 ++trace_states;
@@ -1012,7 +1090,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         }
                     }
                 }
-                if (train && term) pair_clear(p, pc, lane, tcnt);
+                if (train && term) {
+                    pair_clear(p, pc, lane, tcnt);
+#pragma unroll
+                    for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
+                }
             } else if constexpr (PAIRS) {
                 if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
                 pair_sweep(p, pc, lane, train ? tcnt : 0u, [&](uint32_t id, bool first, double ev) {
@@ -1164,6 +1246,20 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
 __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, INSTR>(p);
+}
+// Eligibility traces on the small tables (FrozenLake, CliffWalking: the pair
+// bitmap) in groups of <= 256 lanes, at most 2 groups per CU (cfg 4: 2^17 lanes in
+// 512 groups): 2 waves per SIMD is all the lanes give, so a wave may hold 256
+// VGPRs — the sweep's interleaved rounds and the bitmap stay in registers instead
+// of the 128-VGPR bound's scratch spills
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_train_shared_w(KParams p) {
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false>(p);
+}
+template <int ENV, int AGENT, int POLICY>
+constexpr bool use_w() {
+    return RLAMD_TRACES_W && AGENT == RL_AGENT_TRACES && POLICY != RL_POLICY_NEURAL &&
+           (ENV == RL_ENV_CLIFF_WALKING || ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED);
 }
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
@@ -1479,6 +1575,10 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
             }
           }
           if (!k) k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+        } else if constexpr (use_w<ENV, AGENT, POLICY>()) {
+            // 256 CUs: <= 512 groups keeps the grid at <= 2 groups (2 waves per SIMD) per CU
+            k = (block.x <= 256 && grid.x <= 512) ? (const void *)k_train_shared_w<ENV, AGENT, POLICY, SEL, ALGO>
+                                                  : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         } else {
             k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         }
