@@ -347,6 +347,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
                            // (measured equal on cfg 4 once the bitmap and opq() removed the
                            // scratch arrays: 0.8875 vs 0.8869 ms, so off)
 #endif
+#ifndef RLAMD_OWNER_SCAN
+#define RLAMD_OWNER_SCAN 1   // pair-trace sweep: item owners by ballot + readlane scan (0: shuffle binary search)
+#endif
 #ifndef RLAMD_PAIR_TC
 #define RLAMD_PAIR_TC 8   // HBM pair slots per batch of the sweep (loads issued together)
 #endif
@@ -1033,10 +1036,37 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 // waves per SIMD (cfg 4) the rounds' LDS / HBM round trips overlap
                 // instead of queueing one dependent chain per round
                 constexpr uint32_t U = RLAMD_SWEEP_U;
+                const bool nonempty = npl != 0u;
                 for (uint32_t q0 = 0; q0 < T; q0 += 64u * U) {
-                    uint32_t qv[U], lo[U];
+                    uint32_t qv[U], lo[U], exo[U];
 #pragma unroll
-                    for (uint32_t u = 0; u < U; ++u) { qv[u] = q0 + 64u * u + lid; lo[u] = 0; }
+                    for (uint32_t u = 0; u < U; ++u) { qv[u] = q0 + 64u * u + lid; lo[u] = 0; exo[u] = 0; }
+#if RLAMD_OWNER_SCAN
+                    // owner of item q: the last non-empty lane with excl <= q.  The owner of
+                    // q0 from one ballot; then the few non-empty lanes whose lists start inside
+                    // this iteration's items, in lane order, by readlane (scalar, no LDS
+                    // round trip): a short uniform loop instead of 6 dependent shuffles
+                    {
+                        const uint32_t qend = q0 + 64u * U - 1u;
+                        const uint64_t m0 = __ballot(nonempty && excl <= q0);
+                        const uint32_t own0 = 63u - (uint32_t)__builtin_clzll(m0);   // q0 < T: m0 != 0
+                        const uint32_t ex0 = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)own0);
+#pragma unroll
+                        for (uint32_t u = 0; u < U; ++u) { lo[u] = own0; exo[u] = ex0; }
+                        uint64_t m = __ballot(nonempty && excl > q0 && excl <= qend);
+                        while (m) {
+                            const uint32_t jl = (uint32_t)__builtin_ctzll(m);
+                            m &= m - 1ull;
+                            const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)jl);
+#pragma unroll
+                            for (uint32_t u = 0; u < U; ++u) {
+                                const bool in = e <= qv[u];
+                                lo[u] = in ? jl : lo[u];
+                                exo[u] = in ? e : exo[u];
+                            }
+                        }
+                    }
+#else
 #pragma unroll
                     for (uint32_t st = 32; st; st >>= 1) {   // owner: last lane with excl <= q
 #pragma unroll
@@ -1045,12 +1075,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             if (e <= qv[u]) lo[u] += st;
                         }
                     }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) exo[u] = (uint32_t)__shfl((int)excl, (int)lo[u], 64);
+#endif
                     uint32_t jv[U], utv[U], wv[U], colv[U], hidv[U];
                     uint64_t lanev[U];
                     double tdv[U], evv[U];
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
-                        jv[u] = qv[u] - (uint32_t)__shfl((int)excl, (int)lo[u], 64);
+                        jv[u] = qv[u] - exo[u];
                         tdv[u] = __shfl(td, (int)lo[u], 64);
                         utv[u] = P == 2 ? (uint32_t)__shfl((int)ut, (int)lo[u], 64) : 0u;
                         hidv[u] = PBITS ? (uint32_t)__shfl((int)hid, (int)lo[u], 64) : 0xffffu;
