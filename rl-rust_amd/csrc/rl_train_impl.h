@@ -353,6 +353,16 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 #ifndef RLAMD_PAIR_TC
 #define RLAMD_PAIR_TC 8   // HBM pair slots per batch of the sweep (loads issued together)
 #endif
+// HBM pair slots (those past the LDS cache): lane-major, [lane][j] with stride S*A
+// (the longest list), so the consecutive items of one lane a sweep round takes
+// are contiguous — one or two cache lines instead of one line per item
+#ifndef RLAMD_PAIR_LANE_MAJOR
+#define RLAMD_PAIR_LANE_MAJOR 1   // 0: slot-major [j][lane]
+#endif
+__device__ __forceinline__ uint64_t pslot(const KParams &p, uint32_t j, uint64_t lane) {
+    if constexpr (RLAMD_PAIR_LANE_MAJOR) return lane * (uint64_t)(p.S * p.A) + j;
+    else return (uint64_t)j * p.L + lane;
+}
 struct PairCache {
     uint16_t *TRI;
     double *TRE;
@@ -387,8 +397,8 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
     }
     if (np > c.cap) {                               // overflow part: slot_of lookup
         const uint32_t j = p.slot_of[(uint64_t)id * Ls + lane];
-        if (j >= c.cap && j < np && (p.tlist[(uint64_t)j * Ls + lane] & 0x7fffu) == id) {
-            double *e = &p.trace[(uint64_t)j * Ls + lane];
+        if (j >= c.cap && j < np && (p.tlist[pslot(p, j, lane)] & 0x7fffu) == id) {
+            double *e = &p.trace[pslot(p, j, lane)];
             *e = *e + 1.0;
             return;
         }
@@ -402,9 +412,9 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
         const uint32_t vb = *vw, bit = 1u << (s & 31u);
         const bool first = !same_state && (vb & bit) == 0u;
         if ((vb & bit) == 0u) *vw = vb | bit;
-        p.tlist[(uint64_t)j * Ls + lane] = (uint16_t)(id | (first ? 0x8000u : 0u));
+        p.tlist[pslot(p, j, lane)] = (uint16_t)(id | (first ? 0x8000u : 0u));
         p.slot_of[(uint64_t)id * Ls + lane] = (uint16_t)j;
-        p.trace[(uint64_t)j * Ls + lane] = 1.0;
+        p.trace[pslot(p, j, lane)] = 1.0;
     }
 }
 // the sweep over pairs [0, np): fn(pair id, first-of-state, E); E *= gamma*lambda.
@@ -432,21 +442,20 @@ __device__ __forceinline__ void pair_sweep(const KParams &p, const PairCache &c,
         }
     }
     constexpr uint32_t TC = RLAMD_PAIR_TC;
-    const uint64_t Ls = p.L;
     for (uint32_t j0 = c.cap; j0 < np; j0 += TC) {
         uint32_t w[TC];
         double ev[TC];
 #pragma unroll
         for (uint32_t k = 0; k < TC; ++k) {
             const uint32_t j = j0 + k < np ? j0 + k : j0;
-            w[k] = p.tlist[(uint64_t)j * Ls + lane];
-            ev[k] = p.trace[(uint64_t)j * Ls + lane];
+            w[k] = p.tlist[pslot(p, j, lane)];
+            ev[k] = p.trace[pslot(p, j, lane)];
         }
 #pragma unroll
         for (uint32_t k = 0; k < TC; ++k) {
             if (j0 + k < np) {
                 fn(w[k] & 0x7fffu, (w[k] & 0x8000u) != 0u, ev[k]);
-                p.trace[(uint64_t)(j0 + k) * Ls + lane] = ev[k] * p.gl;
+                p.trace[pslot(p, j0 + k, lane)] = ev[k] * p.gl;
             }
         }
     }
@@ -462,15 +471,15 @@ __device__ __forceinline__ void pair_clear(const KParams &p, const PairCache &c,
 __device__ __forceinline__ void pair_cache_load(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
     const uint32_t nl = np < c.cap ? np : c.cap;
     for (uint32_t j = 0; j < nl; ++j) {
-        c.TRI[c.ix(j)] = p.tlist[(uint64_t)j * p.L + lane];
-        c.TRE[c.ix(j)] = p.trace[(uint64_t)j * p.L + lane];
+        c.TRI[c.ix(j)] = p.tlist[pslot(p, j, lane)];
+        c.TRE[c.ix(j)] = p.trace[pslot(p, j, lane)];
     }
 }
 __device__ __forceinline__ void pair_cache_store(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
     const uint32_t nl = np < c.cap ? np : c.cap;
     for (uint32_t j = 0; j < nl; ++j) {
-        p.tlist[(uint64_t)j * p.L + lane] = c.TRI[c.ix(j)];
-        p.trace[(uint64_t)j * p.L + lane] = c.TRE[c.ix(j)];
+        p.tlist[pslot(p, j, lane)] = c.TRI[c.ix(j)];
+        p.trace[pslot(p, j, lane)] = c.TRE[c.ix(j)];
     }
 }
 
@@ -635,7 +644,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         static_assert(A == 4, "a state's pair bits sit in one bitmap word");
         if (active)
             for (uint32_t j = 0; j < tcnt; ++j)
-                pbits_set((j < pc.cap ? (uint32_t)pc.TRI[pc.ix(j)] : (uint32_t)p.tlist[(uint64_t)j * p.L + lane]) &
+                pbits_set((j < pc.cap ? (uint32_t)pc.TRI[pc.ix(j)] : (uint32_t)p.tlist[pslot(p, j, lane)]) &
                           0x7fffu);
     }
 
@@ -1008,8 +1017,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                                 pc.TRI[pc.ix(j)] = tag;
                                 pc.TRE[pc.ix(j)] = 1.0;
                             } else {
-                                p.tlist[(uint64_t)j * p.L + lane] = tag;
-                                p.trace[(uint64_t)j * p.L + lane] = 1.0;
+                                p.tlist[pslot(p, j, lane)] = tag;
+                                p.trace[pslot(p, j, lane)] = 1.0;
                             }
                             pbits_set(id);
                         }
@@ -1030,7 +1039,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
                 const uint32_t excl = incl - npl;
                 const uint32_t T = (uint32_t)__shfl((int)incl, 63, 64);
-                const uint64_t Ls = p.L;
                 // RLAMD_SWEEP_U rounds per iteration, every stage interleaved across
                 // them (owner searches, gathers, loads, then the updates): with 2
                 // waves per SIMD (cfg 4) the rounds' LDS / HBM round trips overlap
@@ -1095,8 +1103,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         wv[u] = 0; evv[u] = 0.0;
                         if (qv[u] < T) {
                             const bool in_lds = jv[u] < pc.cap;
-                            wv[u] = in_lds ? (uint32_t)pc.TRI[colv[u]] : (uint32_t)p.tlist[(uint64_t)jv[u] * Ls + lanev[u]];
-                            evv[u] = in_lds ? pc.TRE[colv[u]] : p.trace[(uint64_t)jv[u] * Ls + lanev[u]];
+                            wv[u] = in_lds ? (uint32_t)pc.TRI[colv[u]] : (uint32_t)p.tlist[pslot(p, jv[u], lanev[u])];
+                            evv[u] = in_lds ? pc.TRE[colv[u]] : p.trace[pslot(p, jv[u], lanev[u])];
                         }
                     }
 #pragma unroll
@@ -1119,7 +1127,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
                             const double en = ev * p.gl;
                             if (in_lds) pc.TRE[col] = en;
-                            else p.trace[(uint64_t)j * Ls + lanev[u]] = en;
+                            else p.trace[pslot(p, j, lanev[u])] = en;
                         }
                     }
                 }
