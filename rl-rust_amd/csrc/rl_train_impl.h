@@ -90,13 +90,15 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     (void)n_start;
     l.cdf = off;
     // trc_kb KiB per group (KParams::trc_kb), at most S*A slots per lane
+    // row strides padded by 2 / 1 entries (PairCache): one lane's consecutive
+    // slots then sit in different LDS banks
     if (shared_q && traces == 2) {
-        const uint32_t c = trc_kb * 1024u / (nthr * 10u);
+        const uint32_t c = trc_kb * 1024u / ((nthr + 2u) * 2u + (nthr + 1u) * 8u);
         l.trc_cap = c < S * A ? c : S * A;
     } else {
         l.trc_cap = 0u;
     }
-    l.trc = off; off += l.trc_cap ? align16(l.trc_cap * nthr * 2u) + l.trc_cap * nthr * 8u : 0u;
+    l.trc = off; off += l.trc_cap ? align16(l.trc_cap * (nthr + 2u) * 2u) + l.trc_cap * (nthr + 1u) * 8u : 0u;
     l.total = off;
     return l;
 }
@@ -367,7 +369,13 @@ struct PairCache {
     uint16_t *TRI;
     double *TRE;
     uint32_t cap, nthr, tid;
-    __device__ __forceinline__ uint32_t ix(uint32_t j) const { return j * nthr + tid; }
+    // slot j of thread t: ids in rows of nthr + 2 u16, E in rows of nthr + 1 f64 —
+    // unpadded, a lane's slots j, j+1, ... (what one sweep round reads) were
+    // 2 KiB apart for 256 threads, i.e. all in one LDS bank
+    __device__ __forceinline__ uint32_t ixi_t(uint32_t j, uint32_t t) const { return j * (nthr + 2u) + t; }
+    __device__ __forceinline__ uint32_t ixe_t(uint32_t j, uint32_t t) const { return j * (nthr + 1u) + t; }
+    __device__ __forceinline__ uint32_t ixi(uint32_t j) const { return ixi_t(j, tid); }
+    __device__ __forceinline__ uint32_t ixe(uint32_t j) const { return ixe_t(j, tid); }
 };
 // E[s][a] += 1: find the pair or append it
 template <int A>
@@ -382,7 +390,7 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
     for (uint32_t j0 = 0; j0 < nl; j0 += TB) {
         uint32_t w[TB];
 #pragma unroll
-        for (uint32_t k = 0; k < TB; ++k) w[k] = c.TRI[c.ix(j0 + k < nl ? j0 + k : j0)] & 0x7fffu;
+        for (uint32_t k = 0; k < TB; ++k) w[k] = c.TRI[c.ixi(j0 + k < nl ? j0 + k : j0)] & 0x7fffu;
 #pragma unroll
         for (uint32_t k = 0; k < TB; ++k) {
             if (j0 + k < nl) {
@@ -392,7 +400,7 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
         }
     }
     if (hit != 0xffffffffu) {
-        c.TRE[c.ix(hit)] += 1.0;
+        c.TRE[c.ixe(hit)] += 1.0;
         return;
     }
     if (np > c.cap) {                               // overflow part: slot_of lookup
@@ -405,8 +413,8 @@ __device__ __forceinline__ void pair_visit(const KParams &p, const PairCache &c,
     }
     const uint32_t j = np++;
     if (j < c.cap) {
-        c.TRI[c.ix(j)] = (uint16_t)(id | (same_state ? 0u : 0x8000u));
-        c.TRE[c.ix(j)] = 1.0;
+        c.TRI[c.ixi(j)] = (uint16_t)(id | (same_state ? 0u : 0x8000u));
+        c.TRE[c.ixe(j)] = 1.0;
     } else {
         uint32_t *vw = &p.vbits[(uint64_t)(s >> 5) * Ls + lane];
         const uint32_t vb = *vw, bit = 1u << (s & 31u);
@@ -430,14 +438,14 @@ __device__ __forceinline__ void pair_sweep(const KParams &p, const PairCache &c,
 #pragma unroll
         for (uint32_t k = 0; k < TL; ++k) {
             const uint32_t j = j0 + k < nl ? j0 + k : j0;
-            w[k] = c.TRI[c.ix(j)];
-            ev[k] = c.TRE[c.ix(j)];
+            w[k] = c.TRI[c.ixi(j)];
+            ev[k] = c.TRE[c.ixe(j)];
         }
 #pragma unroll
         for (uint32_t k = 0; k < TL; ++k) {
             if (j0 + k < nl) {
                 fn(w[k] & 0x7fffu, (w[k] & 0x8000u) != 0u, ev[k]);
-                c.TRE[c.ix(j0 + k)] = ev[k] * p.gl;
+                c.TRE[c.ixe(j0 + k)] = ev[k] * p.gl;
             }
         }
     }
@@ -471,15 +479,15 @@ __device__ __forceinline__ void pair_clear(const KParams &p, const PairCache &c,
 __device__ __forceinline__ void pair_cache_load(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
     const uint32_t nl = np < c.cap ? np : c.cap;
     for (uint32_t j = 0; j < nl; ++j) {
-        c.TRI[c.ix(j)] = p.tlist[pslot(p, j, lane)];
-        c.TRE[c.ix(j)] = p.trace[pslot(p, j, lane)];
+        c.TRI[c.ixi(j)] = p.tlist[pslot(p, j, lane)];
+        c.TRE[c.ixe(j)] = p.trace[pslot(p, j, lane)];
     }
 }
 __device__ __forceinline__ void pair_cache_store(const KParams &p, const PairCache &c, uint64_t lane, uint32_t np) {
     const uint32_t nl = np < c.cap ? np : c.cap;
     for (uint32_t j = 0; j < nl; ++j) {
-        p.tlist[pslot(p, j, lane)] = c.TRI[c.ix(j)];
-        p.trace[pslot(p, j, lane)] = c.TRE[c.ix(j)];
+        p.tlist[pslot(p, j, lane)] = c.TRI[c.ixi(j)];
+        p.trace[pslot(p, j, lane)] = c.TRE[c.ixe(j)];
     }
 }
 
@@ -615,7 +623,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         else return N[idx];
     };
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
-    const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * nthr * 2u)),
+    const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * (nthr + 2u) * 2u)),
                        lay.trc_cap, nthr, tid};
     if constexpr (PAIRS) { if (active) pair_cache_load(p, pc, lane, tcnt); }
     // small tables (S*A <= 256: FrozenLake, CliffWalking): the lane's visited-pair set
@@ -644,7 +652,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         static_assert(A == 4, "a state's pair bits sit in one bitmap word");
         if (active)
             for (uint32_t j = 0; j < tcnt; ++j)
-                pbits_set((j < pc.cap ? (uint32_t)pc.TRI[pc.ix(j)] : (uint32_t)p.tlist[pslot(p, j, lane)]) &
+                pbits_set((j < pc.cap ? (uint32_t)pc.TRI[pc.ixi(j)] : (uint32_t)p.tlist[pslot(p, j, lane)]) &
                           0x7fffu);
     }
 
@@ -1014,8 +1022,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             const uint16_t tag = (uint16_t)(id | (first ? 0x8000u : 0u));
                             const uint32_t j = tcnt++;
                             if (j < pc.cap) {
-                                pc.TRI[pc.ix(j)] = tag;
-                                pc.TRE[pc.ix(j)] = 1.0;
+                                pc.TRI[pc.ixi(j)] = tag;
+                                pc.TRE[pc.ixe(j)] = 1.0;
                             } else {
                                 p.tlist[pslot(p, j, lane)] = tag;
                                 p.trace[pslot(p, j, lane)] = 1.0;
@@ -1096,15 +1104,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         utv[u] = P == 2 ? (uint32_t)__shfl((int)ut, (int)lo[u], 64) : 0u;
                         hidv[u] = PBITS ? (uint32_t)__shfl((int)hid, (int)lo[u], 64) : 0xffffu;
                         lanev[u] = lane - lid + lo[u];        // lanes of a wave are consecutive
-                        colv[u] = jv[u] * nthr + wbase + lo[u];
+                        colv[u] = wbase + lo[u];   // the owner's thread: its slot column
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
                         wv[u] = 0; evv[u] = 0.0;
                         if (qv[u] < T) {
                             const bool in_lds = jv[u] < pc.cap;
-                            wv[u] = in_lds ? (uint32_t)pc.TRI[colv[u]] : (uint32_t)p.tlist[pslot(p, jv[u], lanev[u])];
-                            evv[u] = in_lds ? pc.TRE[colv[u]] : p.trace[pslot(p, jv[u], lanev[u])];
+                            wv[u] = in_lds ? (uint32_t)pc.TRI[pc.ixi_t(jv[u], colv[u])] : (uint32_t)p.tlist[pslot(p, jv[u], lanev[u])];
+                            evv[u] = in_lds ? pc.TRE[pc.ixe_t(jv[u], colv[u])] : p.trace[pslot(p, jv[u], lanev[u])];
                         }
                     }
 #pragma unroll
@@ -1126,7 +1134,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
                             if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
                             const double en = ev * p.gl;
-                            if (in_lds) pc.TRE[col] = en;
+                            if (in_lds) pc.TRE[pc.ixe_t(j, col)] = en;
                             else p.trace[pslot(p, j, lanev[u])] = en;
                         }
                     }
