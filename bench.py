@@ -114,7 +114,8 @@ def cpu_baseline(args):
              (n_episodes 1e5, src/bin/frozen_lake.rs:35-73), 1 core; whole training
              runs repeated (train -> reset, as the bins' sweep) until the sample
              lasts about `cpu_seconds`.
-    multi_core — the same, one independent env per thread (16: the box's share).
+    multi_core — the same, one independent env per thread, on every core the
+             process may use (len(os.sched_getaffinity(0)), recorded in `cores`).
     cfg1   — SURVEY cfg 1: FrozenLake 4x4 one-step Q-learning eps-greedy, 1 core.
     ref_dense — the oracle's dense-array restatement of the same loop, 1 core.
     Non-FrozenLake workloads report ref_dense only (ref_faithful covers FrozenLake).
@@ -154,7 +155,9 @@ def cpu_baseline(args):
                 "sample": f"{what}: {reps} x train({n} episodes, eval every {eval_at}) per core = "
                           f"{r['steps']} training env-steps in {r['seconds']:.2f} s"}
 
-    threads = min(16, os.cpu_count() or 1)     # the box's CPU share; os.cpu_count() is the machine
+    # every core this process may run on (the box's share: sched_getaffinity, not
+    # os.cpu_count(), which counts the whole machine)
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     fl = args.env == "frozen_lake" and args.agent == "one_step" and args.policy == "tabular"
     desc = (f"{args.env}{' 8x8' if args.map8x8 else ''}{' slippery' if args.slippery else ''} "
             f"{args.agent} {args.algo} {args.selector}")
@@ -218,13 +221,17 @@ def main():
     elif dist_on:
         delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
+        agent.set_merge_groups(world * ((args.lanes + args.group - 1) // args.group))
+    mw = agent.delta_max_words()
 
     def step():
-        if delta is None:                   # launch + merge (librlamd: RCCL all-reduce when world > 1)
+        if delta is None:                   # launch + merge (librlamd: RCCL all-reduces when world > 1)
             agent.run(1)
             return
-        agent.launch_train()                # rehearsal: torch all_reduce of the delta
-        dist.all_reduce(delta)
+        agent.launch_train()                # rehearsal: torch all_reduces of the merge buffer
+        dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
+        agent.launch_fold()
+        dist.all_reduce(delta[mw:])
         agent.launch_apply()
 
     for _ in range(args.warmup):
@@ -276,10 +283,24 @@ def main():
     # VALU instruction per SIMD).  Cross-check: SQ_INSTS_VALU x 4 cycles matches the
     # kernel's cycles on cfg 2 / 5, i.e. these kernels are VALU-issue bound
     issue = (pmc.get("valu_busy_rocm") or pmc.get("valu_busy_frac")) if pmc else None
+    priced = achieved / HBM_PEAK
+    traffic_frac = (traffic / avg_kern_s / HBM_PEAK) if traffic else None
+    q_repr = agent.q_repr()
+    # the binding limit measured by the PMC passes: VALU issue when it is closer
+    # to its ceiling than the HBM traffic is to its own
+    valu_bound = issue is not None and traffic_frac is not None and issue > traffic_frac
+    hbm_priced = {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": priced,
+                  "basis": "SURVEY 8(d) algorithmic bytes per env-step x env-steps per launch / kernel time"}
+    if valu_bound:
+        roof = {"bound": "valu", "achieved": issue, "peak": 1.0, "unit": "VALU-busy fraction", "frac": issue}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": priced}
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": ("f64 TD arithmetic; shared Q int64 fixed point 2^-40 (range proven, |Q| <= 2048, no clamp)"
+                  if q_repr == "fixed40" else f"f64 TD arithmetic; shared Q f64 ({q_repr}: the reference's full range)"),
         "data": "synthetic (env lanes seeded per global lane id; no dataset)",
         "config": {"workload": f"run mode (rl_agent_run: lanes train continuously, eval interleave off) "
                                f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
@@ -291,18 +312,16 @@ def main():
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
                    "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"
                                   else "torch all_reduce (rehearsal)") if dist_on else "none",
-                   "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"]},
-        # `frac` prices SURVEY §8(d)'s algorithmic bytes (32 B/env-step) against HBM
-        # peak; the fused kernel keeps lane records in registers for K steps, so the
-        # PMC-measured traffic is far below them and the binding limit is on-chip
-        # issue / LDS: `traffic_frac` (measured bytes) and `issue_frac` (VALU busy)
-        # say how close each is to its own ceiling.
-        "roofline": {"bound": "hbm", "basis": "priced algorithmic bytes (SURVEY 8(d)), not measured traffic",
-                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                     "traffic": traffic,
-                     "traffic_frac": (traffic / avg_kern_s / HBM_PEAK) if traffic else None,
-                     "issue_frac": issue,
+                   "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"],
+                   "q_repr": q_repr},
+        "build": rlamd.lib().rl_build_info().decode(),
+        # `roofline` names the measured binder (PMC passes, profiles/counters.json):
+        # `issue_frac` VALU busy, `traffic_frac` the measured HBM bytes against the
+        # peak; `hbm_priced` prices SURVEY §8(d)'s algorithmic bytes (32 B/env-step:
+        # the fused kernel keeps lane records in registers for K steps, so the
+        # measured traffic is far below them)
+        "roofline": {**roof, "traffic": traffic, "traffic_frac": traffic_frac, "issue_frac": issue,
+                     "hbm_priced": hbm_priced, "priced_frac": priced,
                      "issue_basis": "VALU busy = SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles) (ROCm VALUBusy)",
                      "counters": pmc.get("source") if pmc else None,
                      "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
@@ -310,11 +329,6 @@ def main():
                      "bytes_per_launch": bytes_per_launch, "bytes_per_env_step": bytes_per_step,
                      **({"trace_v_bar": v_bar} if args.agent == "traces" else {})},
         "torch_event_ms": ev0.elapsed_time(ev1),
-        # shared-mode fixed-point health over the timed window: Q entries the
-        # |Q| <= 2048 clamp held, TD deltas saturated at +-2^51 raw (0 = the run
-        # is the reference's f64 arithmetic)
-        "q_clamp_hits": st1["q_clamp_hits"] - st0["q_clamp_hits"],
-        "delta_saturations": st1["delta_saturations"] - st0["delta_saturations"],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 3
+#define RL_ABI_VERSION 4
 
 enum rl_status {
     RL_OK = 0,
@@ -80,6 +80,23 @@ enum rl_decay_kind {    /* the epsilon_decay closure: `a - d` (src/bin/frozen_la
     RL_DECAY_LINEAR = 0, RL_DECAY_MUL = 1
 };
 enum rl_lane_mode { RL_MODE_TRAIN = 0, RL_MODE_EVAL = 1, RL_MODE_DONE = 2 };
+/* How a shared-mode (group_size > 1) Q table is held (rl_agent_q_repr):
+ *   RL_QREPR_FIXED40: int64 fixed point, value = raw * 2^-40 — only where the
+ *       host proves |Q| stays within 2048 (one-step agent, single table, a
+ *       bootstrap that is a sub-convex combination of Q values: SARSA, Q-learning,
+ *       expected SARSA over eps-greedy), so no update is ever clamped;
+ *   RL_QREPR_F64: the reference's f64 with its whole range (+-inf, NaN included:
+ *       the double policy's A - B grows by (1 + lr) per update pair,
+ *       double_tabular_policy.rs:50-57; UCB + expected SARSA reaches NaN);
+ *   RL_QREPR_PRIVATE: group_size 1, each lane an f64 reference agent.
+ * A step's simultaneous contributions to one entry are combined order-free:
+ * their mean, with the sum formed exactly on the integer grid of the largest
+ * one (one contribution: exactly Q += lr * td, tabular_policy.rs:35-38). */
+enum rl_q_repr { RL_QREPR_FIXED40 = 0, RL_QREPR_F64 = 1, RL_QREPR_PRIVATE = 2 };
+enum rl_q_mode {        /* rl_agent_set_q_mode */
+    RL_QMODE_AUTO = 0,  /* the fixed point where proven (and the table is exact in it), else f64 */
+    RL_QMODE_F64 = 1    /* f64 always */
+};
 
 /* Env constructor arguments: FrozenLakeEnv::new(map, is_slippery, max_steps)
  * (src/env/frozen_lake.rs:48), CliffWalkingEnv::new(max_steps) (cliff_walking.rs:34),
@@ -161,10 +178,10 @@ typedef struct rl_stats {
     uint64_t launches;
     uint64_t trace_states;    /* traces agents: sum over training steps of the visited-set size
                                  swept by the eligibility update (mean = V-bar of SURVEY 8(d)) */
-    /* shared mode (fixed-point Q, value = raw * 2^-40, |raw| <= 2^51): deviations from
-     * the reference's unbounded f64 Q.  0 means every update was exact. */
-    uint64_t q_clamp_hits;    /* entry updates (step settle or merge) clamped at |Q| = 2048 */
-    uint64_t delta_saturations; /* per-lane deltas lr*td saturated at |d| = 2048 */
+    /* ABI v3 counted updates clamped to a fixed-point range; since v4 no range is
+     * ever clamped (rl_q_repr), so both stay 0 */
+    uint64_t q_clamp_hits;
+    uint64_t delta_saturations;
 } rl_stats;
 
 typedef struct rl_env rl_env;
@@ -174,6 +191,8 @@ typedef struct rl_comm rl_comm;
 /* ---------------------------------------------------------------- misc */
 const char *rl_last_error(void);
 int rl_abi_version(void);
+/* how this librlamd.so was built: compiler flags, target, experiment switches */
+const char *rl_build_info(void);
 int rl_device_count(int *count);
 /* usize observation id of the reference's Blackjack env: fxhash 0.2.1 of
  * BlackJackObservation{p_score,d_score,p_ace} (src/env/blackjack.rs:25-27). */
@@ -228,8 +247,14 @@ int rl_agent_stats(rl_agent *a, rl_stats *out);
  * double policy (alpha, beta).  n = number of doubles in out. */
 int rl_agent_get_q(rl_agent *a, double *out, size_t n);
 int rl_agent_set_q(rl_agent *a, const double *in, size_t n);
-/* shared mode only: raw fixed-point Q (value = raw * 2^-40) */
+/* shared mode only: the raw words of Q — the fixed-point integers (value = raw *
+ * 2^-40) or the f64 bits (NaN canonical 0x7FF8000000000000), per rl_agent_q_repr */
 int rl_agent_get_q_raw(rl_agent *a, int64_t *out, size_t n);
+/* the shared Q representation now (rl_q_repr) */
+int rl_agent_q_repr(rl_agent *a, int32_t *repr);
+/* request a representation (rl_q_mode).  Switching to f64 is exact; AUTO goes
+ * back to the fixed point only when the proof holds and every value is exact in it. */
+int rl_agent_set_q_mode(rl_agent *a, int32_t mode);
 /* UCB counters (upper_confidence_bound.rs:11-12, u128 there; u64 here: 2^64
  * selections of one entry is out of reach): shared [S][A] + t[1];
  * private [n_lanes][S][A] + t[n_lanes] */
@@ -283,9 +308,12 @@ int rl_agent_set_weights(rl_agent *a, const double *in, size_t n);
 int rl_net_features(const rl_env_config *env, int32_t input, double *out, size_t n);
 
 /* -------- multi-GPU (SURVEY 8(b) rl_sync, 8(e)): one process per GPU, lanes
- * partitioned contiguously (lane_offset = rank * n_lanes).  The ONLY collective is
- * an RCCL int64 sum of the merge delta (ΔQ, group counts, ΔN, Δt, flag counts)
- * over xGMI after every launch; integer sums make Q identical for any rank count.
+ * partitioned contiguously (lane_offset = rank * n_lanes).  The only collectives
+ * are RCCL int64 all-reduces of the merge buffer over xGMI after every launch:
+ * f64 Q: a MAX over its first rl_agent_delta_max_words words (per-entry grid
+ * codes), then a SUM over the rest (grid sums, group counts, ΔN, Δt, NaN/inf
+ * counts); fixed point: the SUM only.  Integer sums make Q identical for any
+ * rank count at a fixed global lane set.
  * Bootstrap: rank 0 calls rl_comm_unique_id and hands the bytes to every rank
  * (any channel: MPI, a file, the launcher), then each rank calls rl_comm_init. */
 #define RL_COMM_ID_BYTES 128
@@ -302,14 +330,22 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c);
  * communicator (none: this rank alone) on the agent's stream, then Q_base += Δ */
 int rl_agent_sync(rl_agent *a);
 
-/* -------- multi-GPU: the ΔQ merge as an external collective (shared mode) */
-/* number of int64 words of the merge delta (ΔQ, ΔN, Δt, Δflags) */
+/* -------- multi-GPU: the merge as an external collective (shared mode) */
+/* int64 words of the merge buffer (all of it) and of its leading MAX part */
 int rl_agent_delta_words(rl_agent *a, uint64_t *n);
-/* use caller-owned device memory (e.g. a torch int64 tensor, zeroed) as the delta */
+int rl_agent_delta_max_words(rl_agent *a, uint64_t *n);
+/* use caller-owned device memory (e.g. a torch int64 tensor, zeroed) as the buffer */
 int rl_agent_set_delta_buffer(rl_agent *a, void *device_ptr, uint64_t n_words);
-/* one launch = train kernel (writes this device's ΔQ into the delta buffer) ... */
+/* learner groups over every rank (the f64 merge grid's headroom; the attached
+ * communicator sets it, external collectives call this); 0 = this rank's */
+int rl_agent_set_merge_groups(rl_agent *a, uint64_t total_groups);
+/* one launch = train kernel (this device's part of the buffer) ...
+ * [caller all-reduces the MAX words with MAX] ... */
 int rl_agent_launch_train(rl_agent *a);
-/* ... [caller all-reduces the delta buffer across ranks] ... then Q_base += Δ, Δ = 0 */
+/* ... the grid sums (f64; nothing for the fixed point) ... [caller all-reduces the
+ * remaining words with SUM] ... */
+int rl_agent_launch_fold(rl_agent *a);
+/* ... then Q_base = the merged values, buffer zeroed */
 int rl_agent_launch_apply(rl_agent *a);
 /* run on a caller stream (hipStream_t as void*); NULL = the handle's own stream */
 int rl_agent_set_stream(rl_agent *a, void *stream);

@@ -1281,15 +1281,38 @@ uint64_t rlo_faithful_bench(const rlo_config *c, uint64_t n_episodes, uint64_t e
 }
 
 /* ======================================================================== */
-/* 2. batched schedule (the GPU semantics) — fixed-point Q                   */
+/* 2. batched schedule (the GPU semantics)                                   */
 /*                                                                           */
 /* Per learner group g (lanes [g*G, (g+1)*G)) and synchronous step:          */
 /*   R-phase: lanes needing a reset: s=reset(), a=get_action(s)              */
 /*            (UCB: all read N,t; then N[s][a]+=1 per lane, t+=#calls)       */
 /*   S-phase: (s2,r,term)=step(a); a2=get_action(s2) (same UCB snapshot rule) */
-/*            train lanes: td from the Q snapshot, deltas summed, applied at  */
-/*            the end of the step (integer sums: order-free).                */
-/* Every K=sync_every steps: Q_base += sum_g (Q_g - Q_base), same for N, t.  */
+/*            train lanes: td from the Q snapshot; every entry moves by the   */
+/*            MEAN of the contributions it received, at the end of the step. */
+/* Every K=sync_every steps the groups merge: each entry takes the mean over  */
+/* the groups that changed it; UCB N and t are summed.                       */
+/*                                                                           */
+/* Two representations of the shared Q (rlo_batch_q_repr):                   */
+/*  FIXED40: int64 fixed point 2^-40, only where the range proof holds        */
+/*           (o_delta_bound: one-step agent, single table, contracting       */
+/*           bootstrap) — there |Q| never leaves max(|Q0|, R/(1-gamma)) and  */
+/*           no clamp can engage.                                            */
+/*  F64:     Q is f64 with the reference's full range (no clamp: entries      */
+/*           that the reference drives to +-inf / NaN get there too,         */
+/*           double_tabular_policy.rs:50-57).  A step's            */
+/*           contributions d_i (f64, = lr*td or lr*(td*E)) to one entry are   */
+/*           summed EXACTLY on the integer grid 2^e of the largest one        */
+/*           (fq_step_combine): e = max(code(d_i), 1) - 1075 (code = biased   */
+/*           exponent), so the largest is exact and the rest are rounded to   */
+/*           its ulp; the sum is an int64 (order free, as on the GPU), the    */
+/*           entry moves by ldexp(fl((double)sum * fl(1/n)), e).  n == 1 is   */
+/*           exact: one lane reproduces Q[s][a] += lr*td                      */
+/*           (tabular_policy.rs:35-38).  Any NaN / +-inf contribution makes   */
+/*           the step's move NaN / +-inf (IEEE sum algebra).  Traces use one  */
+/*           grid per group step, from the largest |td| and the trace bound. */
+/*           The merge takes the mean of the changed groups' VALUES on the   */
+/*           same kind of grid (plus headroom bits for many groups).  NaN is  */
+/*           stored canonical (0x7FF8...), so equal states compare bitwise.  */
 /* ======================================================================== */
 typedef struct {
     rlo_rng rng;
@@ -1340,6 +1363,18 @@ struct rlo_batch {
     double *feat, *w_g;  /* input features [S][in]; current lane's parameters */
     uint32_t net_gen;
     uint64_t last_done;  /* lanes DONE at the end of the last launch (rl_stats::done_lanes) */
+    /* shared-Q representation (see the section header) */
+    int qrepr;           /* RLO_QREPR_FIXED40 / RLO_QREPR_F64 */
+    int q_forced;        /* rlo_batch_set_q_mode: 0 auto, 1 F64, 2 F64 with sequential sums */
+    double q_abs0;       /* max |Q| at the last reset / set_q (the range proof's Q0) */
+    double *qd_base, *qd_grp; /* F64: [P][S][A] merged base / the running group's copy (qd_g points at it) */
+    uint32_t *ck; double *cd; size_t cn, ccap;   /* F64: this step's contributions (entry, d), lane order */
+    uint32_t *fcode;     /* F64: per-entry max code of the step / merge */
+    double *fseq;        /* F64 sequential variant: per-entry running sums */
+    uint32_t td_code;    /* F64 traces: max code of the finite td of the group step */
+    int trace_k;         /* F64 traces: 2^trace_k >= |lr| * (trace bound) * (1 + 2^-50) */
+    uint64_t merge_groups;   /* learner groups over all ranks (merge grid headroom) */
+    double *gvals;       /* F64 merge: every local group's Q after its launch [g][P][S][A] */
 };
 
 /* Fixed-point Q (shared mode).  |Q raw| <= 2^51, so every entry converts to
@@ -1359,7 +1394,6 @@ static int64_t q_fix_sat(double d, uint8_t *flag, int *sat) {
     x = fmin(x, D_RAW_MAX);
     return (int64_t)rint(x);
 }
-static int64_t q_fix(double d, uint8_t *flag) { return q_fix_sat(d, flag, NULL); }
 static inline int64_t q_clamp(int64_t v) {
     return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
 }
@@ -1377,6 +1411,133 @@ static inline double q_val(int64_t raw, uint8_t fl) {
 }
 static inline int64_t wrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
+/* ---- F64 shared Q (section header above) ---- */
+#define QNAN_BITS 0x7FF8000000000000ull
+static inline uint64_t u_of(double x) { dbits b; b.d = x; return b.u; }
+static inline double d_of(uint64_t u) { dbits b; b.u = u; return b.d; }
+static inline double canon_nan(double x) { return x != x ? d_of(QNAN_BITS) : x; }
+/* biased exponent field: 0 for zero / subnormal, 2047 for inf / NaN */
+static inline uint32_t f64_code(double x) { return (uint32_t)(u_of(x) >> 52) & 0x7ffu; }
+static inline uint8_t nf_flag(double x) { return x != x ? QF_NAN : (x > 0.0 ? QF_PINF : QF_NINF); }
+/* the IEEE sum of contributions with these non-finite kinds */
+static inline double nf_value(uint8_t f) {
+    if ((f & QF_NAN) || ((f & QF_PINF) && (f & QF_NINF))) return d_of(QNAN_BITS);
+    return (f & QF_PINF) ? INFINITY : -INFINITY;
+}
+/* d on the grid 2^e, rounded half-to-even (|result| < 2^53 when |d| < 2^(e+53)) */
+static inline int64_t fq_raw(double d, int e) { return (int64_t)rint(ldexp(d, -e)); }
+/* the mean of n grid values summing to `sum` */
+static inline double fq_mean(int64_t sum, uint64_t n, int e) { return ldexp((double)sum * (1.0 / (double)n), e); }
+static inline int fq_grid(uint32_t code) { return (int)(code > 1u ? code : 1u) - 1075; }
+static int ceil_log2_u64(uint64_t n) {
+    int h = 0;
+    while (h < 64 && ((uint64_t)1 << h) < n) ++h;
+    return h;
+}
+/* merge grid headroom: n values of < 2^(53-h) grid units stay below 2^63 for
+ * up to 2^(10+h) groups (rlamd rl_host.cpp merge_headroom) */
+static int fq_merge_headroom(uint64_t groups) {
+    const int h = ceil_log2_u64(groups) - 10;
+    return h > 0 ? h : 0;
+}
+/* traces grid: every contribution fl(lr * fl(td * E)) of a group step is below
+ * 2^(max(code(td),1) - 1022 + k) with 2^k >= |lr| * Ebound * (1 + 2^-50), where
+ * Ebound bounds an accumulating trace (elegibility_traces_agent.rs:75-96: E += 1
+ * on a visit, E *= gamma*lambda after each sweep): 1/(1-|gl|) for |gl| < 1, else
+ * the geometric sum over the longest episode.  Same formula as the product's
+ * host (rl_host.cpp trace_grid_k). */
+int rlo_trace_grid_k(double lr, double gamma, double lambda_, uint32_t max_steps, int32_t env) {
+    const double gl = gamma * lambda_, a = fabs(gl);
+    double eb;
+    if (a < 1.0) {
+        eb = 1.0 / (1.0 - a);
+    } else {
+        const uint32_t T = env == RLO_ENV_BLACKJACK ? 32u : max_steps + 1u;
+        double p = 1.0;
+        eb = 0.0;
+        for (uint32_t k = 0; k <= T && eb < INFINITY; ++k) { eb += p; p *= a; }
+    }
+    const double x = fabs(lr) * eb * (1.0 + 0x1p-50) * 1.0001;
+    if (!(x > 0.0)) return 0;
+    if (!(x < INFINITY)) return 1100;
+    int ex;
+    (void)frexp(x, &ex);
+    return ex < -1100 ? -1100 : (ex > 1100 ? 1100 : ex);
+}
+/* a value the fixed point holds exactly and in range */
+static inline int fix_exact(double v) {
+    if (!(fabs(v) <= 2048.0)) return 0;
+    const double x = v * 0x1p40;
+    return x == rint(x);
+}
+
+/* ---- the range proof that admits the fixed point (rlamd rl_host.cpp delta_bound,
+ * same conditions): the one-step agent on a single table, with a bootstrap that
+ * is a sub-convex combination of Q values (SARSA's pick, Q-learning's max,
+ * expected SARSA over eps-greedy), keeps every entry within
+ * max(|Q0|, R/(1-gamma)); the double policy (double_tabular_policy.rs:50-57,
+ * A - B grows by (1 + lr) per update pair), eligibility traces and UCB +
+ * expected SARSA (u_i / sum(u) weights) are not contractions. */
+static double o_reward_bound(int env) {
+    switch (env) {
+    case RLO_ENV_FROZEN_LAKE: return 1.0;
+    case RLO_ENV_FROZEN_LAKE_EDITED: return 10.0;
+    case RLO_ENV_CLIFF_WALKING: return 100.0;
+    case RLO_ENV_TAXI: return 20.0;
+    case RLO_ENV_BLACKJACK: return 1.0;
+    default: return INFINITY;
+    }
+}
+static double o_delta_bound(const rlo_batch *b) {
+    const rlo_config *c = &b->c;
+    if (b->priv || b->feat) return INFINITY;
+    if (c->agent != RLO_AGENT_ONE_STEP || c->policy != RLO_POLICY_TABULAR) return INFINITY;
+    if (c->selector == RLO_SEL_UCB && c->algo == RLO_ALGO_EXPECTED_SARSA) return INFINITY;
+    const double lr = c->lr, g = c->gamma;
+    if (!(lr >= 0.0 && g >= 0.0 && g < 1.0 && isfinite(b->q_abs0))) return INFINITY;
+    if (!(lr <= 1.0)) return INFINITY;
+    if (c->selector == RLO_SEL_EPS_GREEDY && c->algo == RLO_ALGO_EXPECTED_SARSA) {
+        const int dec = c->decay_kind == RLO_DECAY_MUL ? (c->eps_decay >= 0.0 && c->eps_decay <= 1.0)
+                                                       : c->eps_decay >= 0.0;
+        if (!(c->eps0 >= 0.0 && c->eps0 <= 1.0 && c->eps_final >= 0.0 && dec)) return INFINITY;
+    }
+    const double R = o_reward_bound(c->env);
+    const double mb = b->q_abs0 > R / (1.0 - g) ? b->q_abs0 : R / (1.0 - g);
+    if (!(mb <= 2000.0)) return INFINITY;
+    const double ep_len = c->env == RLO_ENV_BLACKJACK ? 1.0 : (double)c->max_steps + 1.0;
+    if (!(ep_len * R * 65536.0 < 0x1p50)) return INFINITY;
+    return lr * (R + (1.0 + g) * mb);
+}
+static int o_proven(const rlo_batch *b) { return o_delta_bound(b) < 2000.0; }
+
+/* representation changes: fixed point -> f64 is exact (|raw| <= 2^51) */
+static void o_to_f64(rlo_batch *b) {
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    for (size_t k = 0; k < nq; ++k) b->qd_base[k] = q_val(b->q_base[k], b->f_base[k]);
+    b->qrepr = RLO_QREPR_F64;
+}
+/* qd_base holds a freshly set table: the fixed point when it is allowed and exact */
+static void o_choose_repr(rlo_batch *b) {
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    b->qrepr = RLO_QREPR_F64;
+    if (b->priv || b->q_forced || !o_proven(b)) return;
+    for (size_t k = 0; k < nq; ++k)
+        if (!fix_exact(b->qd_base[k])) return;
+    for (size_t k = 0; k < nq; ++k) { b->q_base[k] = (int64_t)(b->qd_base[k] * 0x1p40); b->f_base[k] = 0; }
+    b->qrepr = RLO_QREPR_FIXED40;
+}
+static void o_set_abs0(rlo_batch *b, const double *v, size_t n) {
+    b->q_abs0 = 0.0;
+    for (size_t k = 0; k < n; ++k) {
+        const double a = fabs(v[k]);
+        b->q_abs0 = a != a ? INFINITY : (a > b->q_abs0 ? a : b->q_abs0);
+    }
+}
+/* after a selector / algorithm change: a fixed-point table whose proof no longer holds goes f64 */
+static void o_recheck_repr(rlo_batch *b) {
+    if (!b->priv && b->qrepr == RLO_QREPR_FIXED40 && !o_proven(b)) o_to_f64(b);
+}
+
 static void b_row(const rlo_batch *b, uint32_t tbl, uint32_t s, double *out) {
     size_t base = ((size_t)tbl * b->S + s) * b->A;
     if (b->feat) {                    /* NeuralPolicy::get_values / predict (neural_policy.rs:43-53) */
@@ -1384,7 +1545,7 @@ static void b_row(const rlo_batch *b, uint32_t tbl, uint32_t s, double *out) {
         net_forward(&b->net, b->w_g, b->feat + (size_t)s * b->net.in, opre, out);
         return;
     }
-    if (b->priv) {
+    if (b->priv || b->qrepr == RLO_QREPR_F64) {
         for (uint32_t i = 0; i < b->A; ++i) out[i] = b->qd_g[base + i];
         return;
     }
@@ -1451,6 +1612,10 @@ rlo_batch *rlo_batch_create(const rlo_config *c) {
     b->acc_c = (int64_t *)calloc(nq, 8);
     b->n_base = (uint64_t *)calloc(nsa, 8); b->n_g = b->n_g_own = (uint64_t *)calloc(nsa, 8);
     b->acc_n = (int64_t *)calloc(nsa, 8);
+    b->qd_base = (double *)calloc(nq, 8); b->qd_grp = (double *)calloc(nq, 8);
+    b->fcode = (uint32_t *)calloc(nq, 4); b->fseq = (double *)calloc(nq, 8);
+    b->merge_groups = b->n_groups;
+    b->trace_k = rlo_trace_grid_k(c->lr, c->gamma, c->lambda_, c->max_steps, c->env);
     b->records.esz = sizeof(rlo_record);
     b->lanes = (lane_t *)calloc(c->n_lanes, sizeof(lane_t));
     for (uint32_t i = 0; i < c->n_lanes; ++i) {
@@ -1480,6 +1645,7 @@ void rlo_batch_destroy(rlo_batch *b) {
     free(b->lanes); free(b->q_base); free(b->f_base); free(b->q_g); free(b->f_g); free(b->dq);
     free(b->df); free(b->dc); free(b->acc_c); free(b->acc_q); free(b->acc_f); free(b->n_base); free(b->n_g_own); free(b->acc_n);
     free(b->records.p); free(b->feat);
+    free(b->qd_base); free(b->qd_grp); free(b->fcode); free(b->fseq); free(b->ck); free(b->cd); free(b->gvals);
     free(b);
 }
 /* Agent::reset: policy cleared to the default row, selector state fresh, lane
@@ -1487,9 +1653,9 @@ void rlo_batch_destroy(rlo_batch *b) {
  * double_tabular_policy.rs:62-65 keeps policy_flag). */
 void rlo_batch_reset(rlo_batch *b) {
     size_t nq = (size_t)b->P * b->S * b->A;
-    uint8_t fl = 0;
-    int64_t d = q_clamp(q_fix(b->c.q_default, &fl));
-    for (size_t i = 0; i < nq; ++i) { b->q_base[i] = d; b->f_base[i] = fl; }
+    for (size_t i = 0; i < nq; ++i) b->qd_base[i] = canon_nan(b->c.q_default);
+    o_set_abs0(b, &b->c.q_default, 1);
+    o_choose_repr(b);
     memset(b->n_base, 0, sizeof(uint64_t) * b->S * b->A);
     b->t_base = 1;
     b->net_gen++;
@@ -1518,6 +1684,7 @@ int rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps) {
 void rlo_batch_set_selector(rlo_batch *b, int32_t sel) {
     b->c.selector = sel;
     b->specials = b->c.selector == RLO_SEL_UCB && b->c.algo == RLO_ALGO_EXPECTED_SARSA;
+    o_recheck_repr(b);
     memset(b->n_base, 0, sizeof(uint64_t) * b->S * b->A);
     b->t_base = 1;
     for (uint32_t i = 0; i < b->c.n_lanes; ++i) {
@@ -1528,6 +1695,30 @@ void rlo_batch_set_selector(rlo_batch *b, int32_t sel) {
 void rlo_batch_set_algo(rlo_batch *b, int32_t algo) {
     b->c.algo = algo;
     b->specials = b->c.selector == RLO_SEL_UCB && b->c.algo == RLO_ALGO_EXPECTED_SARSA;
+    o_recheck_repr(b);
+}
+/* RLO_QMODE_AUTO: the fixed point where the range proof holds (and the table is
+ * exact in it), else f64; RLO_QMODE_F64: f64 always; RLO_QMODE_F64_SEQ (oracle
+ * only): f64 with every step / merge sum formed sequentially in lane / group
+ * order instead of on the exponent grid — the drift reference */
+void rlo_batch_set_q_mode(rlo_batch *b, int mode) {
+    if (b->priv) return;
+    b->q_forced = mode;
+    if (mode != RLO_QMODE_AUTO) {
+        if (b->qrepr == RLO_QREPR_FIXED40) o_to_f64(b);
+        return;
+    }
+    if (b->qrepr == RLO_QREPR_F64) {
+        const size_t nq = (size_t)b->P * b->S * b->A;
+        const double keep = b->q_abs0;
+        o_set_abs0(b, b->qd_base, nq);
+        o_choose_repr(b);
+        if (b->qrepr == RLO_QREPR_F64) b->q_abs0 = keep;
+    }
+}
+int rlo_batch_q_repr(const rlo_batch *b) { return b->priv ? RLO_QREPR_PRIVATE : b->qrepr; }
+void rlo_batch_set_merge_groups(rlo_batch *b, uint64_t total_groups) {
+    b->merge_groups = total_groups ? total_groups : b->n_groups;
 }
 void rlo_batch_set_record(rlo_batch *b, int e) { b->record = e; }
 
@@ -1535,6 +1726,17 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
     size_t k = ((size_t)tbl * b->S + s) * b->A + a;
     if (b->priv) {                   /* Q[s][a] += lr*td exactly as tabular_policy.rs:36 */
         b->qd_g[k] += delta;
+        return;
+    }
+    if (b->qrepr == RLO_QREPR_F64) {   /* combined at the end of the step (fq_step_combine) */
+        if (b->cn == b->ccap) {
+            b->ccap = b->ccap ? 2 * b->ccap : 4096;
+            b->ck = (uint32_t *)realloc(b->ck, b->ccap * sizeof(uint32_t));
+            b->cd = (double *)realloc(b->cd, b->ccap * sizeof(double));
+        }
+        b->ck[b->cn] = (uint32_t)k;
+        b->cd[b->cn] = delta;
+        b->cn++;
         return;
     }
     uint8_t fl = 0;
@@ -1556,6 +1758,48 @@ static void add_delta(rlo_batch *b, uint32_t tbl, uint32_t s, uint32_t a, double
 static int64_t mean_delta(int64_t sum, int64_t n) {
     if (n <= 0) return 0;
     return (int64_t)trunc((double)sum * (1.0 / (double)n));
+}
+
+/* F64: the end of a group step.  Per entry, the step's contributions (lane
+ * order in cd[]) are combined order-free: largest code -> grid 2^e, integer sum,
+ * mean; non-finite contributions give the IEEE result.  RLO_QMODE_F64_SEQ sums
+ * the f64 contributions in lane order instead (the drift reference). */
+static void fq_step_combine(rlo_batch *b) {
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    const int traces = b->c.agent == RLO_AGENT_TRACES;
+    const int seq = b->q_forced == RLO_QMODE_F64_SEQ;
+    memset(b->dq, 0, nq * 8);
+    memset(b->dc, 0, nq * 4);
+    memset(b->df, 0, nq);
+    memset(b->fcode, 0, nq * 4);
+    memset(b->fseq, 0, nq * 8);
+    for (size_t i = 0; i < b->cn; ++i) {
+        const uint32_t k = b->ck[i];
+        const double d = b->cd[i];
+        b->dc[k]++;
+        if (!isfinite(d)) b->df[k] |= nf_flag(d);
+        else if (f64_code(d) > b->fcode[k]) b->fcode[k] = f64_code(d);
+    }
+    /* traces: one grid for the group step (the contributions of a row come from
+     * many lanes' sweeps; the bound is known before any is formed) */
+    const int e_tr = fq_grid(b->td_code) + b->trace_k;
+    for (size_t i = 0; i < b->cn; ++i) {
+        const uint32_t k = b->ck[i];
+        const double d = b->cd[i];
+        if (!isfinite(d)) continue;
+        b->dq[k] += fq_raw(d, traces ? e_tr : fq_grid(b->fcode[k]));
+        b->fseq[k] += d;
+    }
+    for (size_t k = 0; k < nq; ++k) {
+        if (!b->dc[k]) continue;
+        double mv;
+        if (b->df[k]) mv = nf_value(b->df[k]);
+        else if (seq) mv = b->fseq[k] * (1.0 / (double)b->dc[k]);
+        else mv = fq_mean(b->dq[k], b->dc[k], traces ? e_tr : fq_grid(b->fcode[k]));
+        b->qd_g[k] = canon_nan(b->qd_g[k] + mv);
+    }
+    b->cn = 0;
+    b->td_code = 0;
 }
 
 /* Policy::update with x = td (one-step) or td * E[o][b] (traces):
@@ -1595,6 +1839,9 @@ static double b_update(rlo_batch *b, lane_t *L, uint32_t s, uint32_t a, double r
     if (b->c.agent == RLO_AGENT_ONE_STEP) {
         b_policy_update(b, ut, s, a, td);
     } else {
+        /* F64 traces: the group step's grid follows its largest finite |td| */
+        if (!b->priv && b->qrepr == RLO_QREPR_F64 && isfinite(td) && f64_code(td) > b->td_code)
+            b->td_code = f64_code(td);
         L->trace[(size_t)s * A + a] += 1.0;
         if (!L->visited[s]) { L->visited[s] = 1; L->vlist[L->vcnt++] = s; }
         for (uint32_t vi = 0; vi < L->vcnt; ++vi) {   /* first-visit order (see f_update) */
@@ -1667,6 +1914,8 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
     memset(b->dq, 0, nq * 8);
     memset(b->dc, 0, nq * 4);
     memset(b->df, 0, nq);
+    b->cn = 0;
+    b->td_code = 0;
     for (uint32_t j = 0; j < nl; ++j) {
         lane_t *L = &b->lanes[lane0 + j];
         rlo_record *R = rec ? &rec[j] : NULL;
@@ -1730,20 +1979,28 @@ static void group_step(rlo_batch *b, uint32_t lane0, uint32_t nl, rlo_record *re
         }
     }
     if (b->priv) return;
+    if (b->qrepr == RLO_QREPR_F64) {
+        fq_step_combine(b);
+        return;
+    }
     for (size_t k = 0; k < nq; ++k) {
         b->q_g[k] = q_clamp_count(b, b->q_g[k] + mean_delta(b->dq[k], b->dc[k]));
         b->f_g[k] |= b->df[k];
     }
 }
 
-/* Merge delta, same layout as the GPU's (rl_kparams.h):
- * [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts] (int64).  It is
- * a plain integer sum over groups, so shards (GPUs) can add theirs with an
- * all-reduce and every rank applies the identical total. */
+/* Merge buffer, same layout as the GPU's (rl_kparams.h): PSA "max" words
+ * [PSA codes] then the "sum" words [PSA sums][PSA group counts][SA dN][1 dt]
+ * [3*PSA flag counts] (int64).  Multi-rank (every rank runs its groups):
+ *   launch_groups -> all-reduce MAX of the max words -> fold -> all-reduce SUM of
+ *   the sum words -> apply_delta
+ * Every rank then applies the identical total.  The fixed point uses only the
+ * sum words (integer sums of the groups' changes; fold is a no-op). */
 uint64_t rlo_batch_delta_words(const rlo_batch *b) {
     const size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
-    return 2 * nq + nsa + 1 + 3 * nq;
+    return nq + 2 * nq + nsa + 1 + 3 * nq;
 }
+uint64_t rlo_batch_delta_max_words(const rlo_batch *b) { return (uint64_t)b->P * b->S * b->A; }
 
 /* run every local group for K synchronous steps and ADD its changes to delta
  * (shared mode); private mode just runs the lanes (delta untouched) */
@@ -1770,11 +2027,15 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
         free(tmp);
         return;
     }
-    int64_t *dsum = delta, *dcnt = delta + nq, *dn = delta + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
+    int64_t *dmax = delta;
+    int64_t *dsum = delta + nq, *dcnt = dsum + nq, *dn = dsum + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
+    const int f64 = b->qrepr == RLO_QREPR_F64;
+    if (f64 && !b->gvals) b->gvals = (double *)malloc(sizeof(double) * nq * b->n_groups);
     for (uint32_t g = 0; g < b->n_groups; ++g) {
         uint32_t lane0 = g * b->G;
         uint32_t nl = b->c.n_lanes - lane0 < b->G ? b->c.n_lanes - lane0 : b->G;
-        memcpy(b->q_g, b->q_base, nq * 8); memcpy(b->f_g, b->f_base, nq);
+        if (f64) { b->qd_g = b->qd_grp; memcpy(b->qd_g, b->qd_base, nq * 8); }
+        else { memcpy(b->q_g, b->q_base, nq * 8); memcpy(b->f_g, b->f_base, nq); }
         memcpy(b->n_g, b->n_base, nsa * 8); b->t_g = b->t_base;
         for (uint32_t k = 0; k < b->K; ++k) {
             group_step(b, lane0, nl, tmp);
@@ -1783,13 +2044,28 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
                 memcpy(dst, tmp, sizeof(rlo_record) * nl);
             }
         }
-        for (size_t i = 0; i < nq; ++i) {
-            const int64_t d = (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]);
-            if (d) { dsum[i] = wrap_add(dsum[i], d); dcnt[i] += 1; }
-            const uint8_t nf = (uint8_t)(b->f_g[i] & ~b->f_base[i]);
-            if (nf & QF_NAN) fc[i] += 1;
-            if (nf & QF_PINF) fc[nq + i] += 1;
-            if (nf & QF_NINF) fc[2 * nq + i] += 1;
+        if (f64) {   /* the group's values stay for the fold; max code / count / kinds now */
+            memcpy(b->gvals + (size_t)g * nq, b->qd_g, nq * 8);
+            for (size_t i = 0; i < nq; ++i) {
+                const double v = b->qd_g[i];
+                if (u_of(v) == u_of(b->qd_base[i])) continue;
+                dcnt[i] += 1;
+                if (!isfinite(v)) {
+                    const uint8_t f = nf_flag(v);
+                    fc[(f == QF_NAN ? 0 : f == QF_PINF ? 1 : 2) * nq + i] += 1;
+                } else if ((int64_t)f64_code(v) > dmax[i]) {
+                    dmax[i] = f64_code(v);
+                }
+            }
+        } else {
+            for (size_t i = 0; i < nq; ++i) {
+                const int64_t d = (int64_t)((uint64_t)b->q_g[i] - (uint64_t)b->q_base[i]);
+                if (d) { dsum[i] = wrap_add(dsum[i], d); dcnt[i] += 1; }
+                const uint8_t nf = (uint8_t)(b->f_g[i] & ~b->f_base[i]);
+                if (nf & QF_NAN) fc[i] += 1;
+                if (nf & QF_PINF) fc[nq + i] += 1;
+                if (nf & QF_NINF) fc[2 * nq + i] += 1;
+            }
         }
         for (size_t i = 0; i < nsa; ++i) dn[i] += (int64_t)(b->n_g[i] - b->n_base[i]);
         *dt += (int64_t)(b->t_g - b->t_base);
@@ -1797,16 +2073,54 @@ void rlo_batch_launch_groups(rlo_batch *b, int64_t *delta) {
     free(tmp);
 }
 
-/* Q_base += mean over groups that changed each entry (clamped); counters summed */
+/* F64 merge, second phase: the local groups' changed finite values on the grid
+ * of the (all-reduced) max code, + headroom bits for the number of groups */
+void rlo_batch_fold(rlo_batch *b, int64_t *delta) {
+    if (b->priv || b->qrepr != RLO_QREPR_F64) return;
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    const int64_t *dmax = delta;
+    int64_t *dsum = delta + nq;
+    const int hb = fq_merge_headroom(b->merge_groups);
+    memset(b->fseq, 0, nq * 8);
+    for (uint32_t g = 0; g < b->n_groups; ++g) {
+        const double *gv = b->gvals + (size_t)g * nq;
+        for (size_t i = 0; i < nq; ++i) {
+            const double v = gv[i];
+            if (u_of(v) == u_of(b->qd_base[i]) || !isfinite(v)) continue;
+            dsum[i] += fq_raw(v, fq_grid((uint32_t)dmax[i]) + hb);
+            b->fseq[i] += v;
+        }
+    }
+}
+
+/* every entry that some group changed takes the mean over those groups
+ * (fixed point: Q_base += mean of the changes; f64: the mean of the values);
+ * UCB counters summed */
 void rlo_batch_apply_delta(rlo_batch *b, const int64_t *delta) {
     size_t nq = (size_t)b->P * b->S * b->A, nsa = (size_t)b->S * b->A;
-    const int64_t *dsum = delta, *dcnt = delta + nq, *dn = delta + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
+    const int64_t *dmax = delta;
+    const int64_t *dsum = delta + nq, *dcnt = dsum + nq, *dn = dsum + 2 * nq, *dt = dn + nsa, *fc = dt + 1;
     if (b->priv) { b->stats[6]++; return; }
-    for (size_t i = 0; i < nq; ++i) {
-        b->q_base[i] = q_clamp_count(b, b->q_base[i] + mean_delta(dsum[i], dcnt[i]));
-        if (fc[i]) b->f_base[i] |= QF_NAN;
-        if (fc[nq + i]) b->f_base[i] |= QF_PINF;
-        if (fc[2 * nq + i]) b->f_base[i] |= QF_NINF;
+    if (b->qrepr == RLO_QREPR_F64) {
+        const int hb = fq_merge_headroom(b->merge_groups);
+        const int seq = b->q_forced == RLO_QMODE_F64_SEQ;
+        for (size_t i = 0; i < nq; ++i) {
+            const uint64_t n = (uint64_t)dcnt[i];
+            if (!n) continue;
+            const uint8_t f = (uint8_t)((fc[i] ? QF_NAN : 0) | (fc[nq + i] ? QF_PINF : 0) | (fc[2 * nq + i] ? QF_NINF : 0));
+            double v;
+            if (f) v = nf_value(f);
+            else if (seq) v = b->fseq[i] * (1.0 / (double)n);
+            else v = fq_mean(dsum[i], n, fq_grid((uint32_t)dmax[i]) + hb);
+            b->qd_base[i] = canon_nan(v);
+        }
+    } else {
+        for (size_t i = 0; i < nq; ++i) {
+            b->q_base[i] = q_clamp_count(b, b->q_base[i] + mean_delta(dsum[i], dcnt[i]));
+            if (fc[i]) b->f_base[i] |= QF_NAN;
+            if (fc[nq + i]) b->f_base[i] |= QF_PINF;
+            if (fc[2 * nq + i]) b->f_base[i] |= QF_NINF;
+        }
     }
     for (size_t i = 0; i < nsa; ++i) b->n_base[i] = b->n_base[i] + (uint64_t)dn[i];
     b->t_base = (uint64_t)((int64_t)b->t_base + *dt);
@@ -1817,6 +2131,7 @@ static void run_launch(rlo_batch *b) {
     const uint64_t nw = rlo_batch_delta_words(b);
     int64_t *delta = (int64_t *)calloc(nw, 8);
     rlo_batch_launch_groups(b, delta);
+    rlo_batch_fold(b, delta);
     rlo_batch_apply_delta(b, delta);
     free(delta);
 }
@@ -1847,7 +2162,7 @@ static void arm_lanes(rlo_batch *b, int mode, uint64_t eval_left) {
     }
 }
 uint64_t rlo_batch_train_episodes(rlo_batch *b, uint64_t n, uint64_t eval_at) {
-    if (n == 0) { arm_lanes(b, RLO_MODE_TRAIN, 0); return 0; }   /* the loop body never runs */
+    if (n == 0) return 0;   /* Agent::train(env, 0, ..) runs no episode (src/agent.rs:80): a no-op */
     b->target_episodes = n; b->eval_at = eval_at; b->eval_only = 0;
     arm_lanes(b, RLO_MODE_TRAIN, 0);
     uint64_t launches = 0;
@@ -1879,28 +2194,34 @@ void rlo_batch_get_q(const rlo_batch *b, double *out) {
         for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(out + i * nq, b->lanes[i].qd, nq * sizeof(double));
         return;
     }
+    if (b->qrepr == RLO_QREPR_F64) { memcpy(out, b->qd_base, nq * 8); return; }
     for (size_t i = 0; i < nq; ++i) out[i] = q_val(b->q_base[i], b->f_base[i]);
 }
-/* Policy contents set by the caller (rl.h rl_agent_set_q): shared mode stores
- * each value as fixed point + sticky flags like the merge base, private mode
- * copies lane tables [L][P][S][A] */
+/* Policy contents set by the caller (rl.h rl_agent_set_q): shared mode keeps
+ * the values in f64, or in the fixed point when the range proof holds and every
+ * value is exact in it (o_choose_repr); private mode copies lane tables [L][P][S][A] */
 void rlo_batch_set_q(rlo_batch *b, const double *in) {
     size_t nq = (size_t)b->P * b->S * b->A;
     if (b->priv) {
         for (uint32_t i = 0; i < b->c.n_lanes; ++i) memcpy(b->lanes[i].qd, in + i * nq, nq * sizeof(double));
         return;
     }
-    for (size_t i = 0; i < nq; ++i) {
-        uint8_t fl = 0;
-        b->q_base[i] = q_clamp(q_fix(in[i], &fl));
-        b->f_base[i] = fl;
-    }
+    for (size_t i = 0; i < nq; ++i) b->qd_base[i] = canon_nan(in[i]);
+    o_set_abs0(b, in, nq);
+    o_choose_repr(b);
 }
+/* raw words: the fixed-point integers, or the f64 bits (canonical NaN) */
 void rlo_batch_get_q_raw(const rlo_batch *b, int64_t *out) {
-    memcpy(out, b->q_base, sizeof(int64_t) * b->P * b->S * b->A);
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    memcpy(out, b->qrepr == RLO_QREPR_F64 ? (const void *)b->qd_base : (const void *)b->q_base, sizeof(int64_t) * nq);
 }
 void rlo_batch_get_qflags(const rlo_batch *b, uint8_t *out) {
-    memcpy(out, b->f_base, (size_t)b->P * b->S * b->A);
+    const size_t nq = (size_t)b->P * b->S * b->A;
+    if (b->qrepr == RLO_QREPR_F64) {
+        for (size_t i = 0; i < nq; ++i) out[i] = isfinite(b->qd_base[i]) ? 0 : nf_flag(b->qd_base[i]);
+        return;
+    }
+    memcpy(out, b->f_base, nq);
 }
 void rlo_batch_get_ucb(const rlo_batch *b, uint64_t *counts, uint64_t *t) {
     if (b->priv) {        /* [L][S][A], t[L] */

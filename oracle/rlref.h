@@ -189,6 +189,20 @@ int    rlo_batch_set_planning(rlo_batch *b, uint32_t planning_steps);
 /* batched schedule option: a lane needing a reset resets, selects (snapshot) and
  * steps in the same synchronous step (record kind 3); shared mode, eps-greedy */
 void   rlo_batch_set_reset_step(rlo_batch *b, int on);
+/* shared-Q representation (rlref.c section 2): the int64 fixed point only where
+ * the range proof holds, else f64 with the reference's full range */
+enum { RLO_QREPR_FIXED40 = 0, RLO_QREPR_F64 = 1, RLO_QREPR_PRIVATE = 2 };
+enum { RLO_QMODE_AUTO = 0, RLO_QMODE_F64 = 1, RLO_QMODE_F64_SEQ = 2 };
+void   rlo_batch_set_q_mode(rlo_batch *b, int mode);
+int    rlo_batch_q_repr(const rlo_batch *b);
+/* learner groups over every rank (the f64 merge grid's headroom); 0 = local */
+void   rlo_batch_set_merge_groups(rlo_batch *b, uint64_t total_groups);
+/* merge buffer: the first rlo_batch_delta_max_words words are all-reduced with MAX
+ * before rlo_batch_fold, the rest with SUM before rlo_batch_apply_delta */
+uint64_t rlo_batch_delta_max_words(const rlo_batch *b);
+void   rlo_batch_fold(rlo_batch *b, int64_t *delta);
+/* traces grid exponent (rlref.c rlo_trace_grid_k) */
+int    rlo_trace_grid_k(double lr, double gamma, double lambda_, uint32_t max_steps, int32_t env);
 
 #ifdef __cplusplus
 }

@@ -380,61 +380,67 @@ __device__ __forceinline__ void ucb_fill(const double (&v)[A], const uint64_t (&
         if ((need >> i) & 1u) u[i] = ucb_value(v[i], c, lnt, (double)n[i]);
 }
 
+// ------------------------------------------------------------------ f64 shared Q
+// The f64 representation of a learner group's Q (KParams::fq; the host picks it
+// wherever the fixed point's range is not proven): entries are the reference's
+// f64 values with its whole range, NaN stored canonical so equal states compare
+// bitwise.  A step's contributions d_i to an entry are summed exactly on the
+// integer grid 2^e of the largest, e = max(code, 1) - 1075 with code = the
+// biased exponent (oracle/rlref.c fq_step_combine).
+constexpr uint64_t QNAN_BITS = 0x7FF8000000000000ull;
+__device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t f64_bits(double x) { return (uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double canon_nan(double x) { return x != x ? as_f64(QNAN_BITS) : x; }
+__device__ __forceinline__ uint32_t f64_code(double x) {
+    return ((uint32_t)((uint64_t)__double_as_longlong(x) >> 52)) & 0x7ffu;
+}
+__device__ __forceinline__ int fq_grid(uint32_t code) { return (int)(code > 1u ? code : 1u) - 1075; }
+// kind of a non-finite value (QF_* bit)
+__device__ __forceinline__ uint32_t nf_flag(double x) { return x != x ? QF_NAN : (x > 0.0 ? QF_PINF : QF_NINF); }
+// the IEEE sum of contributions of these non-finite kinds
+__device__ __forceinline__ double nf_value(uint32_t f) {
+    if ((f & QF_NAN) || ((f & QF_PINF) && (f & QF_NINF))) return as_f64(QNAN_BITS);
+    return (f & QF_PINF) ? __builtin_inf() : -__builtin_inf();
+}
+// d on the grid 2^e, rounded half-to-even; |d| < 2^(e+53) so the result is exact in int64
+__device__ __forceinline__ int64_t fq_raw(double d, int e) {
+    return (int64_t)__builtin_rint(__builtin_ldexp(d, -e));
+}
+// argmax (first maximum, strict >) and max of one f64 row in a single pass
+// (utils.rs:1-21: a NaN at index 0 sticks, later NaNs never win)
+template <int A>
+__device__ __forceinline__ uint32_t argmax_max_f64(const double (&v)[A], double &m) {
+    m = v[0];
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 1; i < A; ++i) {
+        const bool gt = v[i] > m;
+        m = gt ? v[i] : m;
+        r = gt ? (uint32_t)i : r;
+    }
+    return r;
+}
+
 // ------------------------------------------------------------------ fixed-point Q
-// Shared-mode Q entries are int64 fixed point, value = raw * 2^-40, clamped to
-// |raw| <= 2^51 (|Q| <= 2048; |r| <= 100 and gamma = 0.95 keep every reference
-// env's Q within 2000): every entry — and (a+b)/2 of two entries — converts to
-// f64 exactly, so comparisons on raw int64 are identical to the reference's
-// f64 comparisons (argmax / max without conversions).
+// Shared-mode Q entries in the fixed-point representation (only where the host
+// proved the range, rl_host.cpp delta_bound) are int64, value = raw * 2^-40,
+// |raw| <= 2^51 (|Q| <= 2048): every entry — and (a+b)/2 of two entries —
+// converts to f64 exactly, so comparisons on raw int64 are identical to the
+// reference's f64 comparisons (argmax / max without conversions).
 constexpr int64_t Q_RAW_MAX = (int64_t)1 << 51;
 
-// finite delta -> raw: d*2^40 clamped to +-2^51 then rounded half-to-even; the
-// 1.5*2^52 magic add performs rint and the f64->int64 conversion at once.
-// `sat` is set when |d| exceeds the range (rl_stats::delta_saturations).
 // rint(x) as int64 for |x| < 2^51 (the 1.5*2^52 magic add rounds half-to-even)
 __device__ __forceinline__ int64_t rint_i64_small(double x) {
     const double y = x + 0x1.8p52;
     return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
 }
-// q_fix_finite without the range clamp: only where the host proved |d| * 2^40 < 2^51
-// (KParams::hits_zero), so the clamp could not engage
+// delta -> raw units: rint(d * 2^40), exact in range because the host proved
+// |d| * 2^40 < 2^51 wherever the fixed point runs (rl_host.cpp delta_bound)
 __device__ __forceinline__ int64_t q_fix_inrange(double d) { return rint_i64_small(d * 0x1p40); }
-__device__ __forceinline__ int64_t q_fix_finite(double d, bool &sat) {
-    double x = d * 0x1p40;
-    sat = __builtin_fabs(x) > 0x1p51;
-    x = __builtin_fmax(x, -0x1p51);
-    x = __builtin_fmin(x, 0x1p51);
-    const double y = x + 0x1.8p52;
-    return (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
-}
-// with sticky non-finite flags (UCB + expected SARSA)
-__device__ __forceinline__ int64_t q_fix(double d, uint32_t &flag, bool &sat) {
-    sat = false;
-    if (d != d) { flag |= QF_NAN; return 0; }
-    if (d == __builtin_inf()) { flag |= QF_PINF; return 0; }
-    if (d == -__builtin_inf()) { flag |= QF_NINF; return 0; }
-    return q_fix_finite(d, sat);
-}
-__device__ __forceinline__ int64_t q_clamp(int64_t v) {
-    return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
-}
-// clamp with a hit flag (rl_stats::q_clamp_hits): the reference's f64 entry
-// would have left [-2048, 2048] here
-__device__ __forceinline__ int64_t q_clamp(int64_t v, bool &hit) {
-    hit = v > Q_RAW_MAX || v < -Q_RAW_MAX;
-    return v > Q_RAW_MAX ? Q_RAW_MAX : (v < -Q_RAW_MAX ? -Q_RAW_MAX : v);
-}
 // (double)raw * 2^-40 for |raw| <= 2^51 in two operations: raw added to the bits
 // of 1.5*2^12 (whose ulp is 2^-40) gives 6144 + raw*2^-40 exactly, then 6144 off.
 __device__ __forceinline__ double q_val(int64_t raw) {
     return __longlong_as_double((long long)(0x40B8000000000000ull + (uint64_t)raw)) - 6144.0;
-}
-__device__ __forceinline__ double q_val(int64_t raw, uint32_t fl) {
-    if (fl) {
-        if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return __builtin_nan("");
-        return (fl & QF_PINF) ? __builtin_inf() : -__builtin_inf();
-    }
-    return q_val(raw);
 }
 template <int A>
 __device__ __forceinline__ uint32_t argmax_i64(const int64_t (&v)[A]) {
@@ -838,6 +844,14 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
+        v = o > v ? o : v;
+    }
     return v;
 }
 

@@ -287,23 +287,55 @@ double uniform_scale(double low, double high) {
     return scale;
 }
 
-// value of a fixed-point Q entry (matches rlamd::q_val on the device)
-double q_value(int64_t raw, uint32_t fl) {
-    if (fl) {
-        if ((fl & QF_NAN) || ((fl & QF_PINF) && (fl & QF_NINF))) return NAN;
-        return (fl & QF_PINF) ? INFINITY : -INFINITY;
-    }
-    return (double)raw * 0x1p-40;
+// value of a fixed-point Q word (matches rlamd::q_val on the device)
+double q_value(int64_t raw) { return (double)raw * 0x1p-40; }
+uint64_t f64_bits(double x) {
+    uint64_t u;
+    std::memcpy(&u, &x, 8);
+    return u;
 }
-// host twin of rlamd::q_fix + q_clamp (set_q / q_default): clamp +-2^51, rint
-int64_t q_fix(double d, uint32_t &flag) {
-    if (d != d) { flag |= QF_NAN; return 0; }
-    if (d == INFINITY) { flag |= QF_PINF; return 0; }
-    if (d == -INFINITY) { flag |= QF_NINF; return 0; }
-    double x = d * 0x1p40;
-    x = std::fmax(x, -0x1p51);
-    x = std::fmin(x, 0x1p51);
-    return (int64_t)std::rint(x);
+double f64_of(uint64_t u) {
+    double x;
+    std::memcpy(&x, &u, 8);
+    return x;
+}
+// NaN stored canonical (rl_device.h canon_nan): equal states compare bitwise
+uint64_t canon_bits(double x) { return x != x ? 0x7FF8000000000000ull : f64_bits(x); }
+// a value the fixed point holds exactly and within its range
+bool fix_exact(double v) {
+    if (!(std::fabs(v) <= 2048.0)) return false;
+    const double x = v * 0x1p40;
+    return x == std::rint(x);
+}
+// traces grid: every contribution fl(lr * fl(td * E)) of a group step is below
+// 2^(max(code(td),1) - 1022 + k) with 2^k >= |lr| * Ebound * (1 + 2^-50); Ebound
+// bounds an accumulating trace (elegibility_traces_agent.rs:75-96: E += 1 on a
+// visit, E *= gamma*lambda per sweep).  Same formula as the oracle's
+// rlo_trace_grid_k (oracle/rlref.c).
+int trace_grid_k(double lr, double gamma, double lambda, uint32_t max_steps, int env) {
+    const double gl = gamma * lambda, a = std::fabs(gl);
+    double eb;
+    if (a < 1.0) {
+        eb = 1.0 / (1.0 - a);
+    } else {
+        const uint32_t T = env == RL_ENV_BLACKJACK ? 32u : max_steps + 1u;
+        double pw = 1.0;
+        eb = 0.0;
+        for (uint32_t k = 0; k <= T && eb < INFINITY; ++k) { eb += pw; pw *= a; }
+    }
+    const double x = std::fabs(lr) * eb * (1.0 + 0x1p-50) * 1.0001;
+    if (!(x > 0.0)) return 0;
+    if (!(x < INFINITY)) return 1100;
+    int ex;
+    (void)std::frexp(x, &ex);
+    return ex < -1100 ? -1100 : (ex > 1100 ? 1100 : ex);
+}
+// merge grid headroom: n values below 2^(53-h) grid units sum below 2^63 for up
+// to 2^(10+h) groups (oracle fq_merge_headroom)
+int merge_headroom(uint64_t groups) {
+    int h = 0;
+    while (h < 64 && ((uint64_t)1 << h) < groups) ++h;
+    return h - 10 > 0 ? h - 10 : 0;
 }
 
 template <class T>
@@ -363,13 +395,18 @@ struct rl_agent {
     uint4 *core = nullptr, *rng = nullptr, *aux = nullptr;
     double *epi_reward = nullptr;
     // shared
-    int64_t *q_base = nullptr;
-    uint32_t *qf_base = nullptr;
+    int64_t *q_base = nullptr;   // fixed-point words or f64 bits (qrepr)
     uint64_t *n_base = nullptr;
     uint64_t *t_base = nullptr;
-    int64_t *delta_own = nullptr, *delta = nullptr, *delta_rep = nullptr;
-    uint64_t delta_words = 0;
+    // merge buffer [PSA MAX words][delta_words SUM words]: own, or the caller's
+    int64_t *delta_own = nullptr, *delta_max = nullptr, *delta = nullptr, *delta_rep = nullptr;
+    uint64_t delta_words = 0;    // the SUM part
     uint32_t n_rep = 1;
+    uint64_t *qslot = nullptr;   // f64 merge: every group's final Q [n_groups][psal]
+    uint32_t n_groups = 0, psal = 0;
+    uint64_t merge_groups = 0;   // learner groups over every rank
+    int qrepr = RL_QREPR_FIXED40;
+    int q_forced = 0;            // rl_agent_set_q_mode(RL_QMODE_F64)
     // private
     double *q_priv = nullptr;
     uint64_t *n_priv = nullptr;
@@ -407,7 +444,7 @@ struct rl_agent {
     dim3 grid, block;
     size_t smem = 0;
     rl_comm *comm = nullptr;   // multi-GPU: the merge delta is all-reduced over it
-    double q_abs0 = 0.0;       // shared mode: max |Q| the table was last reset / set to (hits_proven_zero)
+    double q_abs0 = 0.0;       // shared mode: max |Q| the table was last reset / set to (delta_bound's Q0)
 };
 
 namespace {
@@ -425,6 +462,7 @@ int agent_select_kernel(rl_agent *a) {
         a->smem = private_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
                                      a->A, (uint32_t)a->eh.cdf.size());
     } else {
+        a->kp.ucb_pack = (uint64_t)a->G * a->K < 65536ull ? 1 : 0;   // UCB + expected SARSA counters (KParams)
         const uint32_t g = std::min(a->G, a->L);
         // lanes per wave (rl_kparams.h KParams::lpw): 64.  RLAMD_LPW=32/16 spreads a
         // group over more waves; measured on cfg 4 (2^17 lanes, 2 waves per SIMD at
@@ -452,7 +490,8 @@ int agent_select_kernel(rl_agent *a) {
             const uint64_t groups = a->grid.x, per_cu = (groups + (uint64_t)ncu - 1) / (uint64_t)ncu;
             const uint64_t resident = std::max<uint64_t>(1, std::min<uint64_t>(per_cu, 2048 / a->block.x));
             const size_t base = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector,
-                                                  a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x, 0);
+                                                  a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x, 0,
+                                                  a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
             const int64_t room = (int64_t)(160 * 1024 / resident) - (int64_t)base - 1024;
             a->kp.trc_kb = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(64, room / 1024));
         }
@@ -461,7 +500,8 @@ int agent_select_kernel(rl_agent *a) {
             if (v >= 0 && v <= 150) a->kp.trc_kb = (uint32_t)v;
         }
         a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo, a->S,
-                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x, a->kp.trc_kb);
+                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x, a->kp.trc_kb,
+                                    a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
         if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
     }
     if (a->tcnt) {
@@ -478,7 +518,9 @@ int agent_select_kernel(rl_agent *a) {
     return RL_OK;
 }
 
-void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f);
+void bj_term_scan(rl_agent *a, const int64_t *q);
+double delta_bound(const rl_agent *a);
+int agent_store_table(rl_agent *a, const double *vals);
 
 int agent_reset_policy(rl_agent *a) {
     const size_t PSA = (size_t)a->P * a->S * a->A, SA = (size_t)a->S * a->A;
@@ -500,23 +542,16 @@ int agent_reset_policy(rl_agent *a) {
             HIPC(hipStreamSynchronize(a->stream));
         }
     } else {
-        uint32_t fl = 0;
-        const int64_t d = q_fix(a->cfg.q_default, fl);
-        a->q_abs0 = std::fabs(a->cfg.q_default);
-        std::vector<int64_t> q(PSA, d);
-        std::vector<uint32_t> f(PSA, fl);
-        HIPC(hipMemcpyAsync(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice, a->stream));
-        HIPC(hipMemcpyAsync(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice, a->stream));
-        HIPC(hipStreamSynchronize(a->stream));
-        bj_term_scan(a, q.data(), f.data());
+        const std::vector<double> v(PSA, a->cfg.q_default);
+        return agent_store_table(a, v.data());
     }
     return RL_OK;
 }
 
 // Blackjack terminal rows (dense obs with player sum > 21 or dealer card > 10:
 // rl_train_impl.h bj_nonterminal) are read-only for the kernels; record whether
-// each table holds one finite value there (KParams::bj_tconst)
-void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f) {
+// each table holds one word there (KParams::bj_tconst)
+void bj_term_scan(rl_agent *a, const int64_t *q) {
     a->kp.bj_tconst = 0;
     if (a->cfg.env.kind != RL_ENV_BLACKJACK || a->priv) return;
     const size_t SA = (size_t)a->S * a->A;
@@ -528,7 +563,6 @@ void bj_term_scan(rl_agent *a, const int64_t *q, const uint32_t *f) {
             if (pl <= 21u && d <= 10u) continue;
             for (uint32_t b = 0; b < a->A; ++b) {
                 const size_t i = t * SA + (size_t)s * a->A + b;
-                if (f[i]) return;
                 if (first) { v[t] = q[i]; first = false; }
                 else if (q[i] != v[t]) return;
             }
@@ -591,7 +625,8 @@ double env_reward_bound(int kind) {
 // UCB + expected SARSA weighs by u_i / sum(u) (upper_confidence_bound.rs:48-63):
 // no bound, its kernels always count.
 // Returns the proven bound on |lr * E * td| (+inf when nothing is proven); the
-// clamp and the delta saturation provably never engage when it is < 2000.
+// fixed point (|Q| <= 2048) is used only when it is < 2000 (fix_proven), every
+// other table is held in f64 (rl.h rl_q_repr).
 double delta_bound(const rl_agent *a) {
     const double inf = std::numeric_limits<double>::infinity();
     const rl_agent_config &c = a->cfg;
@@ -617,13 +652,66 @@ double delta_bound(const rl_agent *a) {
     if (!(ep_len * R * 65536.0 < 0x1p50)) return inf;
     return lr * emax * (R + (1.0 + g) * mb);
 }
-bool hits_proven_zero(const rl_agent *a) { return delta_bound(a) < 2000.0; }
+bool fix_proven(const rl_agent *a) { return delta_bound(a) < 2000.0; }
 // The 8-wave kernels pack a step's contributions to an entry into one int64,
 // sum * 2^11 + count (one LDS atomic per contribution instead of two): exact
 // while at most G contributions of at most delta_bound * 2^40 + 1 raw units each
 // keep |sum| * 2^11 + 2047 below 2^63, i.e. G * delta_bound < 2^12 (FrozenLake and
 // Blackjack at the CLI defaults: 0.15 * 512 and 2.0 * 512)
 bool pack_proven(const rl_agent *a) { return (double)a->G * delta_bound(a) < 4000.0; }
+
+// Write a freshly set table (P*S*A values) as the shared base: in the fixed point
+// when allowed (not forced to f64, the proof holds with Q0 = max |value|, every
+// value exact in it), else as f64 bits (NaN canonical).  Same rule as the
+// oracle's o_choose_repr (oracle/rlref.c).
+int agent_store_table(rl_agent *a, const double *vals) {
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    double amax = 0.0;
+    for (size_t i = 0; i < PSA; ++i) {
+        const double x = std::fabs(vals[i]);
+        amax = x != x ? INFINITY : std::max(amax, x);
+    }
+    a->q_abs0 = amax;
+    bool fix = !a->q_forced && fix_proven(a);
+    for (size_t i = 0; fix && i < PSA; ++i) fix = fix_exact(vals[i]);
+    std::vector<int64_t> w(PSA);
+    for (size_t i = 0; i < PSA; ++i) w[i] = fix ? (int64_t)(vals[i] * 0x1p40) : (int64_t)canon_bits(vals[i]);
+    a->qrepr = fix ? RL_QREPR_FIXED40 : RL_QREPR_F64;
+    HIPC(hipMemcpyAsync(a->q_base, w.data(), PSA * 8, hipMemcpyHostToDevice, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    bj_term_scan(a, w.data());
+    return agent_select_kernel(a);   // the kernel and its LDS carve follow the representation
+}
+// the base's values as f64 (either representation)
+int agent_table_values(rl_agent *a, std::vector<double> &vals, std::vector<int64_t> &w) {
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    w.resize(PSA);
+    vals.resize(PSA);
+    HIPC(hipMemcpyAsync(w.data(), a->q_base, PSA * 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (size_t i = 0; i < PSA; ++i)
+        vals[i] = a->qrepr == RL_QREPR_F64 ? f64_of((uint64_t)w[i]) : q_value(w[i]);
+    return RL_OK;
+}
+// fixed point -> f64 (exact: |raw| <= 2^51)
+int agent_to_f64(rl_agent *a) {
+    std::vector<double> v;
+    std::vector<int64_t> w;
+    int rc = agent_table_values(a, v, w);
+    if (rc) return rc;
+    for (size_t i = 0; i < w.size(); ++i) w[i] = (int64_t)canon_bits(v[i]);
+    HIPC(hipMemcpyAsync(a->q_base, w.data(), w.size() * 8, hipMemcpyHostToDevice, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    a->qrepr = RL_QREPR_F64;
+    bj_term_scan(a, w.data());
+    return agent_select_kernel(a);
+}
+// after a selector / algorithm change: a fixed-point table whose proof no longer
+// holds continues in f64 (the proof follows the table's real state)
+int agent_recheck_repr(rl_agent *a) {
+    if (!a->priv && a->qrepr == RL_QREPR_FIXED40 && !fix_proven(a)) return agent_to_f64(a);
+    return agent_select_kernel(a);
+}
 
 void agent_sync_params(rl_agent *a) {
     KParams &p = a->kp;
@@ -637,9 +725,17 @@ void agent_sync_params(rl_agent *a) {
     p.eps_dm = a->cfg.decay_kind == RL_DECAY_MUL ? a->cfg.eps_decay : 1.0;
     p.eps_ds = a->cfg.decay_kind == RL_DECAY_MUL ? 0.0 : a->cfg.eps_decay;
     p.algo = a->cfg.algo;
-    p.hits_zero = hits_proven_zero(a) ? 1 : 0;
-    p.pack_ok = p.hits_zero && pack_proven(a) ? 1 : 0;
+    p.fq = a->qrepr == RL_QREPR_F64 ? 1 : 0;
+    p.pack_ok = !p.fq && pack_proven(a) ? 1 : 0;
+    p.trace_k = trace_grid_k(a->cfg.lr, a->cfg.gamma, a->cfg.lambda, a->cfg.env.max_steps, a->cfg.env.kind);
+    p.merge_hb = merge_headroom(a->merge_groups);
     p.delta = a->delta;
+    p.delta_max = a->delta_max;
+    p.qslot = a->qslot;
+    p.n_groups = a->n_groups;
+    // LDS-held entries per group: Blackjack eps-greedy keeps the 484 non-terminal rows
+    p.psal = (a->cfg.env.kind == RL_ENV_BLACKJACK && a->cfg.selector != RL_SEL_UCB)
+                 ? a->P * 484u * a->A : a->P * a->S * a->A;
     p.plan_steps = a->plan;
     p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;
     p.elog = a->elog_cap ? a->elog_d : nullptr;
@@ -670,12 +766,15 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
         a->events.emplace_back(e0, e1);
     }
     if (merge) *merge = false;
-    if (!a->priv) {                       // fold the group-delta replicas into the delta
-        if (merge && a->delta == a->delta_own && a->cfg.selector != RL_SEL_UCB && !a->comm) {
-            launch_fold_apply(a->kp, a->stream);   // ... and apply it (eps-greedy: sums + counts only)
+    if (!a->priv) {
+        if (a->qrepr == RL_QREPR_F64) {   // f64 merge, first phase (UCB: ΔN / Δt from the replicas)
+            if (a->cfg.selector == RL_SEL_UCB) launch_fold_replicas(a->kp, a->stream);
+            launch_fq_merge_a(a->kp, a->stream);
+        } else if (merge && a->delta_max == a->delta_own && a->cfg.selector != RL_SEL_UCB && !a->comm) {
+            launch_fold_apply(a->kp, a->stream);   // fold the replicas and apply (eps-greedy: sums + counts only)
             *merge = true;
         } else {
-            launch_fold_replicas(a->kp, a->stream);
+            launch_fold_replicas(a->kp, a->stream);   // fold the group-delta replicas into the delta
         }
         HIPC(hipGetLastError());
     }
@@ -691,22 +790,43 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
     return RL_OK;
 }
 
+// f64 merge, second phase (after the MAX all-reduce): the grid sums; nothing for the fixed point
+int launch_fold_kernel(rl_agent *a) {
+    if (a->priv || a->qrepr != RL_QREPR_F64) return RL_OK;
+    agent_sync_params(a);
+    launch_fq_merge_b(a->kp, a->stream);
+    HIPC(hipGetLastError());
+    return RL_OK;
+}
 int launch_apply_kernel(rl_agent *a) {
     if (a->priv) return RL_OK;
     agent_sync_params(a);
-    const int spec = a->cfg.selector == RL_SEL_UCB && a->cfg.algo == RL_ALGO_EXPECTED_SARSA;
-    launch_apply(a->kp, spec, a->stream);
+    if (a->qrepr == RL_QREPR_F64) launch_fq_apply(a->kp, a->stream);
+    else launch_apply(a->kp, a->stream);
     HIPC(hipGetLastError());
     return RL_OK;
 }
 
-// the merge's collective: this rank's delta (already folded from the group
-// replicas) summed over every rank, in place, on the agent's stream.  Exact
-// int64 sums, so Q is bit-identical for any rank count at a fixed global lane set.
+// the merge's collectives, in place on the agent's stream: the MAX words (f64:
+// per-entry grid codes) and the SUM words (grid sums / ΔQ, group counts, ΔN, Δt,
+// NaN / inf counts) over every rank.  Exact int64 arithmetic, so Q is
+// bit-identical for any rank count at a fixed global lane set.
+int allreduce_max(rl_agent *a) {
+    if (!a->comm || a->qrepr != RL_QREPR_F64) return RL_OK;
+    NCCLC(ncclAllReduce(a->delta_max, a->delta_max, (size_t)a->P * a->S * a->A, ncclInt64, ncclMax, a->comm->comm,
+                        a->stream));
+    return RL_OK;
+}
 int allreduce_delta(rl_agent *a) {
     if (!a->comm) return RL_OK;   // no communicator: this process's delta is the total
     NCCLC(ncclAllReduce(a->delta, a->delta, a->delta_words, ncclInt64, ncclSum, a->comm->comm, a->stream));
     return RL_OK;
+}
+// the merge after a launch: [MAX] -> fold -> [SUM] -> apply
+int merge_after_launch(rl_agent *a) {
+    int rc;
+    if ((rc = allreduce_max(a)) || (rc = launch_fold_kernel(a)) || (rc = allreduce_delta(a))) return rc;
+    return launch_apply_kernel(a);
 }
 // one launch of K steps + the merge (fused fold+apply for a one-process eps-greedy learner)
 int launch_and_merge(rl_agent *a) {
@@ -714,8 +834,7 @@ int launch_and_merge(rl_agent *a) {
     int rc = launch_train_kernel(a, &merged);
     if (rc) return rc;
     if (merged) return RL_OK;
-    if ((rc = allreduce_delta(a))) return rc;
-    return launch_apply_kernel(a);
+    return merge_after_launch(a);
 }
 // sum of a host value over the ranks (1 rank: itself)
 int allreduce_u64(rl_agent *a, uint64_t v, uint64_t *sum) {
@@ -770,6 +889,15 @@ extern "C" {
 
 const char *rl_last_error(void) { return g_err.c_str(); }
 int rl_abi_version(void) { return RL_ABI_VERSION; }
+#ifndef RLAMD_BUILD_FLAGS
+#define RLAMD_BUILD_FLAGS "unknown"
+#endif
+#define RLAMD_STR2(x) #x
+#define RLAMD_STR(x) RLAMD_STR2(x)
+const char *rl_build_info(void) {
+    return "librlamd abi " RLAMD_STR(RL_ABI_VERSION) "; target gfx950; RLAMD_EXP=" RLAMD_STR(RLAMD_EXP)
+           "; flags: " RLAMD_BUILD_FLAGS;
+}
 int rl_device_count(int *count) {
     HIPC(hipGetDeviceCount(count));
     return RL_OK;
@@ -987,12 +1115,16 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
         if ((rc = dalloc(&a->n_priv, SA * L)) || (rc = dalloc(&a->t_priv, L))) return bad(rc);
     } else {
         a->delta_words = 2 * PSA + SA + 1 + 3 * PSA;
-        if ((rc = dalloc(&a->q_base, PSA)) || (rc = dalloc(&a->qf_base, PSA)) || (rc = dalloc(&a->n_base, SA)) ||
-            (rc = dalloc(&a->t_base, 1)) || (rc = dalloc(&a->delta_own, a->delta_words)))
-            return bad(rc);
-        a->delta = a->delta_own;
-        if (hipMemset(a->delta, 0, a->delta_words * 8) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
         const uint32_t n_groups = (a->L + a->G - 1) / a->G;
+        a->n_groups = n_groups;
+        a->merge_groups = n_groups;
+        // merge buffer [PSA MAX words][delta_words SUM words]; f64 slots for every group
+        if ((rc = dalloc(&a->q_base, PSA)) || (rc = dalloc(&a->n_base, SA)) || (rc = dalloc(&a->t_base, 1)) ||
+            (rc = dalloc(&a->delta_own, PSA + a->delta_words)) || (rc = dalloc(&a->qslot, (size_t)n_groups * PSA)))
+            return bad(rc);
+        a->delta_max = a->delta_own;
+        a->delta = a->delta_own + PSA;
+        if (hipMemset(a->delta_own, 0, (PSA + a->delta_words) * 8) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
         a->n_rep = std::min<uint32_t>(64u, n_groups);
         if ((rc = dalloc(&a->delta_rep, a->delta_words * a->n_rep))) return bad(rc);
         if (hipMemset(a->delta_rep, 0, a->delta_words * a->n_rep * 8) != hipSuccess)
@@ -1028,7 +1160,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     KParams &p = a->kp;
     p.L = a->L; p.G = a->G; p.K = a->K; p.S = a->S; p.A = a->A; p.P = a->P;
     p.core = a->core; p.rng = a->rng; p.aux = a->aux; p.epi_reward = a->epi_reward;
-    p.q_base = a->q_base; p.qf_base = a->qf_base; p.n_base = a->n_base; p.t_base = a->t_base;
+    p.q_base = a->q_base; p.n_base = a->n_base; p.t_base = a->t_base;
     p.delta = a->delta;
     p.delta_rep = a->delta_rep;
     p.n_rep = a->n_rep;
@@ -1061,7 +1193,7 @@ void rl_agent_destroy(rl_agent *a) {
     if (a->own_stream) (void)hipStreamSynchronize(a->own_stream);
     for (auto &ev : a->events) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     dfree(a->core); dfree(a->rng); dfree(a->aux); dfree(a->epi_reward);
-    dfree(a->q_base); dfree(a->qf_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own);
+    dfree(a->q_base); dfree(a->n_base); dfree(a->t_base); dfree(a->delta_own); dfree(a->qslot);
     dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
@@ -1074,9 +1206,10 @@ void rl_agent_destroy(rl_agent *a) {
 
 int rl_agent_set_future_q_value_func(rl_agent *a, int32_t algo) {
     if (!a || algo < 0 || algo > 2) return fail(RL_E_ARG, "bad algo");
+    HIPC(hipSetDevice(a->device));
     a->cfg.algo = algo;
     agent_sync_params(a);
-    return agent_select_kernel(a);
+    return agent_recheck_repr(a);
 }
 
 int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double eps_decay, double eps_final,
@@ -1087,7 +1220,7 @@ int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double e
     a->cfg.eps0 = eps0; a->cfg.eps_decay = eps_decay; a->cfg.eps_final = eps_final;
     a->cfg.decay_kind = decay_kind; a->cfg.ucb_c = ucb_c;
     agent_sync_params(a);
-    int rc = agent_select_kernel(a);
+    int rc = agent_recheck_repr(a);
     if (rc) return rc;
     return agent_reset_selector(a);
 }
@@ -1127,9 +1260,10 @@ int rearm_train(rl_agent *a) {
 int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
+    // Agent::train(env, 0, ..) runs no episode (src/agent.rs:80): nothing changes
+    if (n_episodes == 0) return out ? rl_agent_stats(a, out) : RL_OK;
     int rc = clear_traces(a);
     if (rc) return rc;
-    if (n_episodes == 0) return out ? rl_agent_stats(a, out) : RL_OK;
     launch_arm_full(a->kp, RL_MODE_TRAIN, 0, 0, 0.0, a->stream);
     HIPC(hipGetLastError());
     a->kp.target_episodes = n_episodes;
@@ -1244,12 +1378,11 @@ int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
         return RL_OK;
     }
     if (n < PSA) return fail(RL_E_ARG, "output too small: need P*S*A");
-    std::vector<int64_t> q(PSA);
-    std::vector<uint32_t> f(PSA);
-    HIPC(hipMemcpyAsync(q.data(), a->q_base, PSA * 8, hipMemcpyDeviceToHost, a->stream));
-    HIPC(hipMemcpyAsync(f.data(), a->qf_base, PSA * 4, hipMemcpyDeviceToHost, a->stream));
-    HIPC(hipStreamSynchronize(a->stream));
-    for (size_t i = 0; i < PSA; ++i) out[i] = q_value(q[i], f[i]);
+    std::vector<double> v;
+    std::vector<int64_t> w;
+    const int rc = agent_table_values(a, v, w);
+    if (rc) return rc;
+    std::memcpy(out, v.data(), PSA * 8);
     return RL_OK;
 }
 
@@ -1267,16 +1400,30 @@ int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
         return RL_OK;
     }
     if (n < PSA) return fail(RL_E_ARG, "input too small");
-    std::vector<int64_t> q(PSA);
-    std::vector<uint32_t> f(PSA, 0);
-    a->q_abs0 = 0.0;
-    for (size_t i = 0; i < PSA; ++i) {
-        q[i] = q_fix(in[i], f[i]);
-        a->q_abs0 = std::isnan(in[i]) ? std::numeric_limits<double>::infinity() : std::max(a->q_abs0, std::fabs(in[i]));
-    }
-    HIPC(hipMemcpy(a->q_base, q.data(), PSA * 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(a->qf_base, f.data(), PSA * 4, hipMemcpyHostToDevice));
-    bj_term_scan(a, q.data(), f.data());
+    return agent_store_table(a, in);
+}
+
+int rl_agent_q_repr(rl_agent *a, int32_t *repr) {
+    if (!a || !repr) return fail(RL_E_ARG, "null argument");
+    *repr = a->priv ? RL_QREPR_PRIVATE : a->qrepr;
+    return RL_OK;
+}
+
+int rl_agent_set_q_mode(rl_agent *a, int32_t mode) {
+    if (!a || (mode != RL_QMODE_AUTO && mode != RL_QMODE_F64)) return fail(RL_E_ARG, "bad q mode");
+    if (a->priv) return RL_OK;
+    HIPC(hipSetDevice(a->device));
+    a->q_forced = mode == RL_QMODE_F64 ? 1 : 0;
+    if (a->q_forced) return a->qrepr == RL_QREPR_FIXED40 ? agent_to_f64(a) : RL_OK;
+    if (a->qrepr != RL_QREPR_F64) return RL_OK;
+    // AUTO: back to the fixed point when the proof holds for the table as it is now
+    std::vector<double> v;
+    std::vector<int64_t> w;
+    int rc = agent_table_values(a, v, w);
+    if (rc) return rc;
+    const double keep = a->q_abs0;
+    if ((rc = agent_store_table(a, v.data()))) return rc;
+    if (a->qrepr == RL_QREPR_F64) a->q_abs0 = keep;
     return RL_OK;
 }
 
@@ -1447,17 +1594,30 @@ int rl_agent_take_episodes(rl_agent *a, rl_episode_record *out, uint64_t cap, ui
 
 int rl_agent_delta_words(rl_agent *a, uint64_t *n) {
     if (!a || !n) return fail(RL_E_ARG, "null argument");
-    *n = a->delta_words;
+    *n = a->priv ? 0 : (uint64_t)a->P * a->S * a->A + a->delta_words;
+    return RL_OK;
+}
+int rl_agent_delta_max_words(rl_agent *a, uint64_t *n) {
+    if (!a || !n) return fail(RL_E_ARG, "null argument");
+    *n = a->priv ? 0 : (uint64_t)a->P * a->S * a->A;
     return RL_OK;
 }
 
 int rl_agent_set_delta_buffer(rl_agent *a, void *ptr, uint64_t n_words) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (a->priv) return fail(RL_E_STATE, "private mode has no merge");
-    if (ptr == nullptr) { a->delta = a->delta_own; agent_sync_params(a); return RL_OK; }
-    if (n_words < a->delta_words) return fail(RL_E_ARG, "delta buffer too small");
-    a->delta = (int64_t *)ptr;
+    const uint64_t PSA = (uint64_t)a->P * a->S * a->A;
+    int64_t *base = ptr ? (int64_t *)ptr : a->delta_own;
+    if (ptr && n_words < PSA + a->delta_words) return fail(RL_E_ARG, "delta buffer too small");
+    a->delta_max = base;
+    a->delta = base + PSA;
     agent_sync_params(a);
+    return RL_OK;
+}
+
+int rl_agent_set_merge_groups(rl_agent *a, uint64_t total_groups) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    a->merge_groups = total_groups ? total_groups : a->n_groups;
     return RL_OK;
 }
 
@@ -1465,6 +1625,12 @@ int rl_agent_launch_train(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
     return launch_train_kernel(a);
+}
+
+int rl_agent_launch_fold(rl_agent *a) {
+    if (!a) return fail(RL_E_ARG, "null agent");
+    HIPC(hipSetDevice(a->device));
+    return launch_fold_kernel(a);
 }
 
 int rl_agent_launch_apply(rl_agent *a) {
@@ -1520,7 +1686,15 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (c && a->priv) return fail(RL_E_STATE, "private mode (group_size 1) has no merge to reduce");
     if (c && c->device != a->device) return fail(RL_E_ARG, "communicator and agent on different devices");
+    HIPC(hipSetDevice(a->device));
     a->comm = c;
+    // the f64 merge grid's headroom counts the learner groups of every rank
+    uint64_t total = a->n_groups;
+    if (c) {
+        const int rc = allreduce_u64(a, a->n_groups, &total);
+        if (rc) return rc;
+    }
+    a->merge_groups = total;
     return RL_OK;
 }
 
@@ -1528,9 +1702,7 @@ int rl_agent_sync(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (a->priv) return RL_OK;
     HIPC(hipSetDevice(a->device));
-    int rc = allreduce_delta(a);
-    if (rc) return rc;
-    return launch_apply_kernel(a);
+    return merge_after_launch(a);
 }
 
 int rl_agent_set_stream(rl_agent *a, void *stream) {
@@ -1542,7 +1714,7 @@ int rl_agent_set_stream(rl_agent *a, void *stream) {
 int rl_agent_occupancy(rl_agent *a, uint32_t *groups_per_cu, uint64_t *lds_bytes, uint32_t *block_threads) {
     if (!a || !groups_per_cu || !lds_bytes || !block_threads) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));
-    agent_sync_params(a);   // the kernel choice depends on KParams::hits_zero
+    agent_sync_params(a);   // the kernel choice depends on the Q representation (KParams::fq)
     int n = 0;
     HIPC(a->fn(a->kp, a->grid, a->block, a->smem, a->stream, &n));
     *groups_per_cu = (uint32_t)n;

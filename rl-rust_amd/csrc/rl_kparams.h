@@ -12,9 +12,11 @@
 
 namespace rlamd {
 
-// Q fixed point for the shared (group_size > 1) mode: value = raw * 2^-QFRAC.
+// Q fixed point for the shared (group_size > 1) mode where its range is proven:
+// value = raw * 2^-QFRAC.
 constexpr int QFRAC = 40;
-// sticky non-finite flags of a fixed-point Q entry (IEEE sum algebra, order free)
+// kinds of non-finite values (UCB + expected SARSA visible row flags, the f64
+// representation's non-finite step contributions: IEEE sum algebra, order free)
 constexpr uint32_t QF_NAN = 1u, QF_PINF = 2u, QF_NINF = 4u;
 // replicas of the u64[8] stats block (same-address atomics from every block
 // serialise; spreading them over replicas removed ~0.3 ms per launch)
@@ -42,14 +44,22 @@ struct KParams {
     uint4 *aux;
     double *epi_reward;
     // shared mode
-    int64_t *q_base;       // [P][S][A]
-    uint32_t *qf_base;     // [P][S][A]
+    int64_t *q_base;       // [P][S][A]: fixed-point raw words, or f64 bits (fq)
     uint64_t *n_base;      // [S][A] UCB visit counts (u128 in the reference; u64 never wraps in practice)
     uint64_t *t_base;      // [1]
-    int64_t *delta;        // [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
+    int64_t *delta;        // the merge's SUM words: [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
+    int64_t *delta_max;    // the merge's MAX words (f64: per-entry max code over the changed groups) [P*S*A]
     int64_t *delta_rep;    // n_rep replicas of `delta`: group g adds into replica g % n_rep
     uint32_t n_rep;        // (spreads the same-address int64 atomics of the merge)
     uint32_t delta_words;
+    // f64 representation (rl_device.h "f64 shared Q"): every group writes its
+    // final Q (LDS order, psal entries) to qslot[group][psal] for the merge
+    int32_t fq;            // 1: shared Q is f64 (else the proven fixed point)
+    int32_t trace_k;       // traces grid: 2^trace_k >= |lr| * trace bound (rl_host.cpp trace_grid_k)
+    int32_t merge_hb;      // merge grid headroom bits (learner groups over every rank)
+    uint32_t psal;         // LDS-held entries per group (Blackjack eps-greedy: compact rows)
+    uint64_t *qslot;       // [n_groups][psal] f64 bits
+    uint32_t n_groups;
     // private mode (SoA [entry][lane])
     double *q_priv;
     uint64_t *n_priv;      // [S*A][L]
@@ -92,14 +102,13 @@ struct KParams {
     double lr, gamma, gl, eps_decay, eps_final, ucb_c;
     double eps_dm, eps_ds;     // decay as eps * dm - ds (rl_device.h decay_eps)
     int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
-    // the host proved that no shared-mode Q entry can reach the +-2048 clamp and no
-    // TD delta can saturate for these hyper-parameters (rl_host.cpp hits_proven_zero):
-    // the throughput kernels then skip counting rl_stats::q_clamp_hits /
-    // delta_saturations (both provably 0)
-    int32_t hits_zero;
-    // ... and that a step's contributions to an entry fit one int64 as sum * 2^11 +
-    // count (rl_host.cpp pack_proven): the 8-wave kernels then use one LDS atomic each
+    // fixed point only: the host proved that a step's contributions to an entry fit
+    // one int64 as sum * 2^11 + count (rl_host.cpp pack_proven): the 8-wave kernels
+    // then use one LDS atomic each
     int32_t pack_ok;
+    // UCB + expected SARSA: the launch's and the step's counter increments packed in
+    // one u32 per entry (launch << 16 | step), possible while G * K < 2^16
+    int32_t ucb_pack;
     // batched schedule option (rl_agent_set_reset_step; shared mode, eps-greedy):
     // a lane that needs a reset resets, selects and steps in one synchronous step
     int32_t reset_step;
@@ -143,7 +152,7 @@ inline bool layout_sparse_traces(int agent, int sel, int algo, int priv) {
 }
 train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, int priv);
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
-                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb);
+                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack);
 size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
 
 // env-only kernels (batched Env trait) and KAT probes
@@ -155,7 +164,12 @@ void launch_lane_init(int env, const KParams &p, uint64_t seed, uint64_t lane_of
 void launch_arm_full(const KParams &p, int32_t mode, uint32_t eval_left, int restore_eps, double eps0,
                      hipStream_t s);
 void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s);
-void launch_apply(const KParams &p, int specials, hipStream_t s);
+void launch_apply(const KParams &p, hipStream_t s);
+// the f64 merge (rl_misc.hip): per entry max code / counts / kinds over the
+// changed groups, then the grid sums, then base = their mean
+void launch_fq_merge_a(const KParams &p, hipStream_t s);
+void launch_fq_merge_b(const KParams &p, hipStream_t s);
+void launch_fq_apply(const KParams &p, hipStream_t s);
 void launch_fold_replicas(const KParams &p, hipStream_t s);
 void launch_fold_apply(const KParams &p, hipStream_t s);
 void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);

@@ -26,10 +26,11 @@ size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, u
                        A, n_start, 0u).total;
 }
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
-                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb) {
+                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack) {
     const int traces = agent != RL_AGENT_TRACES ? 0 : layout_sparse_traces(agent, sel, algo, 0) ? 2 : 1;
     const int ucb = sel != RL_SEL_UCB ? 0 : algo == RL_ALGO_EXPECTED_SARSA ? 2 : 1;
-    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, ucb, traces, S, A, n_start, nthr, trc_kb).total;
+    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, ucb, traces, S, A, n_start, nthr, trc_kb, fq,
+                       ucb_pack).total;
 }
 
 // ---------------------------------------------------------------- lane init
@@ -116,10 +117,11 @@ void launch_fold_replicas(const KParams &p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- fused fold + apply
-// One-process merge of an eps-greedy learner (the delta holds [PSA sums][PSA
-// counts] only: no UCB counters, no flag counts): entry i sums its two words over
+// One-process merge of an eps-greedy learner in the fixed point (the delta holds
+// [PSA sums][PSA counts] only: no UCB counters): entry i sums its two words over
 // the replicas (4 replica slices per block, as k_fold_replicas), zeroes them and
-// applies k_apply's rule, Q_base[i] += mean.  One launch instead of two.
+// applies k_apply's rule, Q_base[i] += mean (in range: the host's proof).  One
+// launch instead of two.
 __global__ void __launch_bounds__(256) k_fold_apply(KParams p) {
     __shared__ uint64_t part[2][4][64];
     const uint32_t PSA = p.P * p.S * p.A;
@@ -149,9 +151,7 @@ __global__ void __launch_bounds__(256) k_fold_apply(KParams p) {
         const int64_t sum = (int64_t)((uint64_t)d[i] + part[0][0][lw] + part[0][1][lw] + part[0][2][lw] + part[0][3][lw]);
         const int64_t cnt = (int64_t)((uint64_t)d[PSA + i] + part[1][0][lw] + part[1][1][lw] + part[1][2][lw] +
                                       part[1][3][lw]);
-        bool hit;
-        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(sum, cnt), hit);
-        if (hit) atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + ACC_CLAMP], 1ull);
+        p.q_base[i] = p.q_base[i] + mean_delta(sum, cnt);
         d[i] = 0;
         d[PSA + i] = 0;
     }
@@ -162,27 +162,17 @@ void launch_fold_apply(const KParams &p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- merge apply
-// Q_base += Σ_groups ΔQ (already summed by global int64 atomics and, across
-// GPUs, by the caller's all-reduce), then Δ = 0 for the next launch.
-__global__ void k_apply(KParams p, int specials) {
+// Fixed point: Q_base += mean of the groups' (and ranks') ΔQ, already summed by
+// global int64 atomics and, across GPUs, by the caller's all-reduce.  Both
+// representations: UCB counters summed.  Then Δ = 0 for the next launch.
+__global__ void k_apply(KParams p) {
     const uint32_t PSA = p.P * p.S * p.A, SA = p.S * p.A;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     int64_t *d = p.delta;
-    if (i < PSA) {   // Q_base += mean over the groups (and ranks) that changed the entry
-        bool hit;
-        p.q_base[i] = q_clamp(p.q_base[i] + mean_delta(d[i], d[PSA + i]), hit);
-        if (hit) atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + ACC_CLAMP], 1ull);
+    if (i < PSA && !p.fq) {   // Q_base += mean over the groups (and ranks) that changed the entry
+        p.q_base[i] = p.q_base[i] + mean_delta(d[i], d[PSA + i]);
         d[i] = 0;
         d[PSA + i] = 0;
-        if (specials) {
-            int64_t *fc = d + 2 * PSA + SA + 1;
-            uint32_t f = p.qf_base[i];
-            if (fc[i]) f |= QF_NAN;
-            if (fc[PSA + i]) f |= QF_PINF;
-            if (fc[2 * PSA + i]) f |= QF_NINF;
-            p.qf_base[i] = f;
-            fc[i] = fc[PSA + i] = fc[2 * PSA + i] = 0;
-        }
     }
     if (i < SA) {    // UCB counters are counts: summed
         p.n_base[i] = p.n_base[i] + (uint64_t)d[2 * PSA + i];
@@ -193,9 +183,132 @@ __global__ void k_apply(KParams p, int specials) {
         d[2 * PSA + SA] = 0;
     }
 }
-void launch_apply(const KParams &p, int specials, hipStream_t s) {
+void launch_apply(const KParams &p, hipStream_t s) {
     const uint32_t PSA = p.P * p.S * p.A;
-    hipLaunchKernelGGL(k_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p, specials);
+    hipLaunchKernelGGL(k_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p);
+}
+
+// ---------------------------------------------------------------- f64 merge
+// Every group left its final Q (LDS order) in qslot[group][psal].  An entry that
+// some groups changed (bits differ from Q_base) takes the MEAN of their values
+// (oracle rlref.c rlo_batch_launch_groups / _fold / _apply_delta):
+//   a: per entry the max code over the changed finite values (MAX words), the
+//      number of changed groups and of NaN / +inf / -inf values (SUM words);
+//   b: the changed finite values on the grid 2^(max(code,1) - 1075 + merge_hb),
+//      summed (exact int64; merge_hb keeps 2^(10+hb) groups below 2^63);
+//   apply: Q_base = IEEE kind if any non-finite, else ldexp(fl(sum * fl(1/n)), e).
+// Across ranks: MAX all-reduce between a and b, SUM all-reduce between b and apply.
+// Grid: (entry blocks of 64) x (group blocks of 64); 256 threads = 64 entries x
+// 4 group slices of 16 groups.
+__device__ __forceinline__ uint32_t fq_dense(const KParams &p, uint32_t j) {   // LDS index -> dense [P][S][A]
+    if (p.psal == p.P * p.S * p.A) return j;
+    const uint32_t A = p.A, SAL = BJ_LDS_STATES * A, tbl = j / SAL, r = j - tbl * SAL;
+    return tbl * p.S * A + bj_dense(r / A) * A + r % A;
+}
+__global__ void __launch_bounds__(256) k_fq_merge_a(KParams p) {
+    __shared__ uint32_t code[4][64], cnt[4][64], kinds[3][4][64];
+    const uint32_t lw = threadIdx.x & 63u, gs = threadIdx.x >> 6;
+    const uint32_t j = blockIdx.x * 64u + lw;
+    uint32_t c = 0, n = 0, kn = 0, kp = 0, km = 0;
+    if (j < p.psal) {
+        const uint32_t i = fq_dense(p, j);
+        const uint64_t base = (uint64_t)p.q_base[i];
+        const uint32_t g0 = blockIdx.y * 64u + gs * 16u;
+#pragma unroll 4
+        for (uint32_t g = g0; g < g0 + 16u && g < p.n_groups; ++g) {
+            const uint64_t v = p.qslot[(uint64_t)g * p.psal + j];
+            if (v == base) continue;
+            ++n;
+            const double x = as_f64(v);
+            if (__builtin_isfinite(x)) {
+                const uint32_t cd = f64_code(x);
+                c = cd > c ? cd : c;
+            } else {
+                const uint32_t f = nf_flag(x);
+                kn += f == QF_NAN;
+                kp += f == QF_PINF;
+                km += f == QF_NINF;
+            }
+        }
+    }
+    code[gs][lw] = c; cnt[gs][lw] = n; kinds[0][gs][lw] = kn; kinds[1][gs][lw] = kp; kinds[2][gs][lw] = km;
+    __syncthreads();
+    if (gs == 0 && j < p.psal) {
+        const uint32_t i = fq_dense(p, j), PSA = p.P * p.S * p.A;
+        uint32_t cm = 0, nt = 0, k0 = 0, k1 = 0, k2 = 0;
+        for (int q = 0; q < 4; ++q) {
+            cm = code[q][lw] > cm ? code[q][lw] : cm;
+            nt += cnt[q][lw]; k0 += kinds[0][q][lw]; k1 += kinds[1][q][lw]; k2 += kinds[2][q][lw];
+        }
+        if (cm) atomicMax((unsigned long long *)&p.delta_max[i], (unsigned long long)cm);
+        int64_t *d = p.delta, *fc = d + 2 * PSA + p.S * p.A + 1;
+        if (nt) atomicAdd((unsigned long long *)&d[PSA + i], (unsigned long long)nt);
+        if (k0) atomicAdd((unsigned long long *)&fc[i], (unsigned long long)k0);
+        if (k1) atomicAdd((unsigned long long *)&fc[PSA + i], (unsigned long long)k1);
+        if (k2) atomicAdd((unsigned long long *)&fc[2 * PSA + i], (unsigned long long)k2);
+    }
+}
+__global__ void __launch_bounds__(256) k_fq_merge_b(KParams p) {
+    __shared__ int64_t part[4][64];
+    const uint32_t lw = threadIdx.x & 63u, gs = threadIdx.x >> 6;
+    const uint32_t j = blockIdx.x * 64u + lw;
+    int64_t sum = 0;
+    uint32_t i = 0;
+    if (j < p.psal) {
+        i = fq_dense(p, j);
+        const uint64_t base = (uint64_t)p.q_base[i];
+        const int e = fq_grid((uint32_t)p.delta_max[i]) + p.merge_hb;
+        const uint32_t g0 = blockIdx.y * 64u + gs * 16u;
+#pragma unroll 4
+        for (uint32_t g = g0; g < g0 + 16u && g < p.n_groups; ++g) {
+            const uint64_t v = p.qslot[(uint64_t)g * p.psal + j];
+            const double x = as_f64(v);
+            if (v != base && __builtin_isfinite(x)) sum += fq_raw(x, e);
+        }
+    }
+    part[gs][lw] = sum;
+    __syncthreads();
+    if (gs == 0 && j < p.psal) {
+        const int64_t t = part[0][lw] + part[1][lw] + part[2][lw] + part[3][lw];
+        if (t) atomicAdd((unsigned long long *)&p.delta[i], (unsigned long long)t);
+    }
+}
+__global__ void k_fq_apply(KParams p) {
+    const uint32_t PSA = p.P * p.S * p.A, SA = p.S * p.A;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t *d = p.delta, *fc = d + 2 * PSA + SA + 1;
+    if (i < PSA) {
+        const uint64_t n = (uint64_t)d[PSA + i];
+        if (n) {
+            const uint32_t f = (fc[i] ? QF_NAN : 0u) | (fc[PSA + i] ? QF_PINF : 0u) | (fc[2 * PSA + i] ? QF_NINF : 0u);
+            double v;
+            if (f) v = nf_value(f);
+            else v = __builtin_ldexp((double)d[i] * (1.0 / (double)n), fq_grid((uint32_t)p.delta_max[i]) + p.merge_hb);
+            p.q_base[i] = (int64_t)f64_bits(canon_nan(v));
+        }
+        d[i] = 0;
+        d[PSA + i] = 0;
+        fc[i] = fc[PSA + i] = fc[2 * PSA + i] = 0;
+        p.delta_max[i] = 0;
+    }
+    if (i < SA) {
+        p.n_base[i] = p.n_base[i] + (uint64_t)d[2 * PSA + i];
+        d[2 * PSA + i] = 0;
+    }
+    if (i == 0) {
+        p.t_base[0] = (uint64_t)((int64_t)p.t_base[0] + d[2 * PSA + SA]);
+        d[2 * PSA + SA] = 0;
+    }
+}
+void launch_fq_merge_a(const KParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_fq_merge_a, dim3((p.psal + 63) / 64, (p.n_groups + 63) / 64), dim3(256), 0, s, p);
+}
+void launch_fq_merge_b(const KParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_fq_merge_b, dim3((p.psal + 63) / 64, (p.n_groups + 63) / 64), dim3(256), 0, s, p);
+}
+void launch_fq_apply(const KParams &p, hipStream_t s) {
+    const uint32_t PSA = p.P * p.S * p.A;
+    hipLaunchKernelGGL(k_fq_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p);
 }
 
 // ---------------------------------------------------------------- batched Env trait

@@ -19,7 +19,7 @@
 namespace rlamd {
 
 struct SmemLayout {
-    uint32_t st, q, sum, cnt, qf, n, nd, t, list, rcp, tr, cdf, trc, total;
+    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, total;
     uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
@@ -47,11 +47,17 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
     return ((p << 5) + d) * 2u + (row & 1u);
 }
 // LDS carve of one learner group (shared mode) or of the tables only (private).
-//   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40)
-//   sum  int64 [P][S][A]   this step's summed deltas per entry
-//   cnt  u16   [P][S][A]   this step's contributions per entry (u32-word atomics)
-//   qf   u8    [P][S][A]   sticky non-finite flags (UCB + expected SARSA only)
-//   n/t  UCB counters (u64 [S][A], u64 t);  list u16 touched entries + count (traces)
+//   misc u32[4]            f64 traces: the group step's max td code
+//   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40, or f64 bits)
+//   sum  int64 [P][S][A]   this step's summed contributions per entry (integers:
+//                          the fixed point's units, or the f64 entry's grid)
+//   cnt  fixed point: u16 [P][S][A] contributions per entry (u32-word atomics);
+//        f64 one-step: u32 [P][S][A] = max code + 1 << 16 | count; traces: u32
+//        per (table, row) contribution counts
+//   sfl  u8  [P][S][A]     f64: kinds of this step's non-finite contributions
+//                          (UCB + expected SARSA: bits 4-6 of qf instead)
+//   qf   u8  [P][S][A]     UCB + expected SARSA: visible NaN/+-inf kinds of the entries
+//   n/t  UCB counters (u64 [S][A], u64 t);  list u16 touched rows + count (traces)
 //   rcp  f64 [nthr+1]   1.0/n for the combination rule (mean_delta)
 //   tr   env transition table (FrozenLake / CliffWalking; Taxi computes its
 //        transitions and reads its start cdf from HBM, Blackjack has none)
@@ -59,9 +65,11 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 //        list, ids u16 [cap][nthr] then E f64 [cap][nthr] (column = thread)
 // nthr = the shared kernel's block size; 0 for the private kernel (tables only).
 // traces: 0 none, 1 whole-row visited-state sets, 2 visited-pair sets
+// ucb: 0 none, 1 UCB, 2 UCB + expected SARSA (launch counts u32 [S][A] + step
+// counts u16 [S][A], or both in one u32 when ucb_pack)
 __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int traces, uint32_t S,
                                                   uint32_t A, uint32_t n_start, uint32_t nthr,
-                                                  uint32_t trc_kb = 40u) {
+                                                  uint32_t trc_kb = 40u, int fq = 0, int ucb_pack = 0) {
     const int shared_q = nthr != 0;
     SmemLayout l;
     const uint32_t SL = (shared_q && bj_compact(env, ucb)) ? BJ_LDS_STATES : S;   // LDS rows
@@ -71,16 +79,18 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.nrcp = !shared_q ? 0u : (PSA <= nthr ? nthr + 1u : (nthr + 1u < 65u ? nthr + 1u : 65u));
     uint32_t off = 0;
     l.st = off; off += STATS_W * 8u;              // per-block stats accumulators (u64[STATS_W])
+    l.misc = off; off += shared_q ? 16u : 0u;
     l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
-    l.cnt = off; off += shared_q ? align16(((PSA + 1u) / 2u) * 4u) : 0u;
-    l.qf = off; off += (shared_q && ucb) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
-    // UCB counters: u64 N[S][A] (ucb == 1); UCB + expected SARSA (ucb == 2): the
-    // launch's own increments u32 NL[S][A] over the HBM base plus this step's
-    // increments u16 D[S][A] (rl_train_impl.h train_shared_body, SPEC)
+    l.cnt = off; off += shared_q ? align16((fq && !traces) ? PSA * 4u : ((PSA + 1u) / 2u) * 4u) : 0u;
+    l.sfl = off; off += (shared_q && fq && ucb != 2) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
+    l.qf = off; off += (shared_q && ucb == 2) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
     l.n = off;
     l.nd = off + align16(SA * 4u);
-    off += (shared_q && ucb) ? (ucb == 2 ? align16(SA * 4u) + align16(((SA + 1u) / 2u) * 4u) : align16(SA * 8u)) : 0u;
+    off += (shared_q && ucb)
+               ? (ucb == 2 ? (ucb_pack ? align16(SA * 4u) : align16(SA * 4u) + align16(((SA + 1u) / 2u) * 4u))
+                           : align16(SA * 8u))
+               : 0u;
     l.t = off; off += (shared_q && ucb) ? (ucb == 2 ? 32u : 16u) : 0u;   // T[0], T[1] (+ ARR: UCB + ES)
     l.list = off; off += (shared_q && traces) ? align16(PSA * 2u) + 16u : 0u;
     l.rcp = off; off += align16(l.nrcp * 8u);
@@ -491,24 +501,30 @@ __device__ __forceinline__ void pair_cache_store(const KParams &p, const PairCac
     }
 }
 
-// UCB + expected SARSA specials: a step's new NaN/inf flags are ORed into the
-// entry's byte above QF_PENDING while other waves may still read the entry for
-// their TD target; the entry's settle folds them into the visible low bits, so
-// readers see Q_t's flags until the step's barrier (the oracle's df[] applied at
-// step end, rlref.c add_delta).
+// UCB + expected SARSA: the visible NaN/+-inf kinds of every entry (bits 0-2 of
+// QF8, the kinds of the entry's f64 value) let a lane decide the F7 regime from
+// one two-word row read.  A step's non-finite contributions are ORed into bits
+// 4-6 (the f64 step kinds, SFL below) while other waves may still read the row;
+// the entry's settle, after every reader of the step, writes the new value and
+// its visible kinds.
 constexpr uint32_t QF_MASK = QF_NAN | QF_PINF | QF_NINF, QF_PENDING = 4u;
-__device__ __forceinline__ void fold_flags(uint8_t *QF8, uint32_t idx) {
-    const uint32_t f = QF8[idx];
-    if (f >> QF_PENDING) QF8[idx] = (uint8_t)((f | (f >> QF_PENDING)) & QF_MASK);
+__device__ __forceinline__ uint32_t value_flags(double q) { return __builtin_isfinite(q) ? 0u : nf_flag(q); }
+
+// the fixed point is only ever run where the host's range proof can hold
+// (rl_host.cpp delta_bound): one-step agent, single table, contracting bootstrap
+template <int AGENT, int POLICY, int SEL, int ALGO>
+constexpr bool fix_possible() {
+    return AGENT == RL_AGENT_ONE_STEP && POLICY == RL_POLICY_TABULAR &&
+           !(SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA);
 }
 
 // ======================================================================== shared
 // INSTR: step records / episode log compiled in (chosen at launch when either is
 // enabled); the throughput variant carries neither.
-// HITS: count clamp hits / delta saturations (off only where the host proved both 0:
-// KParams::hits_zero)
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, int SLIP = -1, int SWEEP = -1,
-          bool HITS = true, bool PACK = false, int RS = -1>
+// FQ: the group's Q is f64 (rl_device.h "f64 shared Q"); else the fixed point,
+// which the host runs only where it proved the range (no clamp can engage).
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, bool FQ, int SLIP = -1, int SWEEP = -1,
+          bool PACK = false, int RS = -1>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -516,6 +532,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     constexpr bool UCB = SEL == RL_SEL_UCB;
     constexpr bool TRACES = AGENT == RL_AGENT_TRACES;
     constexpr bool SPEC = UCB && ALGO == RL_ALGO_EXPECTED_SARSA;  // inf/NaN possible
+    static_assert(FQ || fix_possible<AGENT, POLICY, SEL, ALGO>(), "no range proof: f64 only");
     constexpr bool BJC = ENV == RL_ENV_BLACKJACK && !UCB;   // compact LDS rows (bj_row)
     const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA;
     const uint32_t SL = BJC ? BJ_LDS_STATES : S, SAL = SL * (uint32_t)A, PSAL = (uint32_t)P * SAL;
@@ -524,16 +541,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     constexpr bool PAIRS = TRACES && !SPEC;            // layout_sparse_traces (rl_kparams.h)
     const SmemLayout lay = smem_layout(ENV, P, UCB ? (SPEC ? 2 : 1) : 0, TRACES ? (PAIRS ? 2 : 1) : 0, S, A, p.n_start,
-                                       nthr, p.trc_kb);
+                                       nthr, p.trc_kb, FQ ? 1 : 0, p.ucb_pack);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
-    uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // two u16 counters per word
+    uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // fixed point: two u16 counters per word
     uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
+    uint32_t *W = (uint32_t *)(smem + lay.cnt);          // f64 one-step: max code + 1 << 16 | count
+    // f64: kinds of the step's non-finite contributions (own bytes; QF's bits 4-6 for SPEC)
+    uint32_t *SFLW = (uint32_t *)(smem + (SPEC ? lay.qf : lay.sfl));
+    uint8_t *SFL8 = (uint8_t *)(smem + (SPEC ? lay.qf : lay.sfl));
+    constexpr uint32_t SFL_SH = SPEC ? QF_PENDING : 0u;
     uint32_t *QF = (uint32_t *)(smem + lay.qf);          // four u8 flag sets per word
     uint8_t *QF8 = (uint8_t *)(smem + lay.qf);
     unsigned long long *N = (unsigned long long *)(smem + lay.n);
     unsigned long long *T = (unsigned long long *)(smem + lay.t);
-    // SPEC counters: n = n_base (HBM, u64) + NL (this launch) [+ D (this step)]
+    // SPEC counters: n = n_base (HBM, u64) + NL (this launch) [+ D (this step)];
+    // ucb_pack: NL = launch << 16 | step in one u32
     uint32_t *NL = (uint32_t *)(smem + lay.n);
     uint32_t *D32 = (uint32_t *)(smem + lay.nd);
     uint16_t *D16 = (uint16_t *)(smem + lay.nd);
@@ -541,6 +564,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint32_t *LISTN = (uint32_t *)(smem + lay.list + align16(PSAL * 2u));
     uint32_t *TR = (uint32_t *)(smem + lay.tr);
     double *RCP = (double *)(smem + lay.rcp);
+    uint32_t *GCODE = (uint32_t *)(smem + lay.misc);
 
     unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
     // LDS table layout: state-major [tbl][s][a] like HBM (LDS_AM = false), or
@@ -568,15 +592,23 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         return qi(tbl, r / (uint32_t)A, r % (uint32_t)A);
     };
     if (tid < STATS_W) ACC[tid] = 0ull;
+    if (tid == 0) GCODE[0] = 0u;
     for (uint32_t i = tid; i < lay.nrcp; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
     for (uint32_t j = tid; j < PSAL; j += nthr) { Q[j] = (unsigned long long)p.q_base[dense_of(j)]; SUM[j] = 0ull; }
-    for (uint32_t i = tid; i < (PSAL + 1u) / 2u; i += nthr) CNT[i] = 0u;
+    if constexpr (FQ && !TRACES) {
+        for (uint32_t j = tid; j < PSAL; j += nthr) W[j] = 0u;
+    } else {
+        for (uint32_t i = tid; i < (PSAL + 1u) / 2u; i += nthr) CNT[i] = 0u;
+    }
+    if constexpr (FQ && !SPEC)
+        for (uint32_t i = tid; i < (PSAL + 3u) / 4u; i += nthr) SFLW[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
-        for (uint32_t i = tid; i < PSA; i += nthr) QF8[lds_of(i)] = (uint8_t)p.qf_base[i];
         if constexpr (SPEC) {
+            for (uint32_t j = tid; j < PSAL; j += nthr) QF8[j] = (uint8_t)value_flags(as_f64(Q[j]));
             for (uint32_t i = tid; i < SA; i += nthr) NL[i] = 0u;
-            for (uint32_t i = tid; i < (SA + 1u) / 2u; i += nthr) D32[i] = 0u;
+            if (!p.ucb_pack)
+                for (uint32_t i = tid; i < (SA + 1u) / 2u; i += nthr) D32[i] = 0u;
         } else {
             for (uint32_t i = tid; i < SA; i += nthr) N[lds_of(i)] = (unsigned long long)p.n_base[i];
         }
@@ -618,9 +650,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // (selection) or with this step's increments (expected SARSA's probabilities)
     auto ucount = [&](uint32_t s, uint32_t i, bool with_step) -> uint64_t {
         const uint32_t idx = qi(0u, s, i);
-        if constexpr (SPEC)
+        if constexpr (SPEC) {
+            if (p.ucb_pack) {
+                const uint32_t w = NL[idx];
+                return p.n_base[s * (uint32_t)A + i] + (uint64_t)(w >> 16) + (with_step ? (uint64_t)(w & 0xffffu) : 0ull);
+            }
             return p.n_base[s * (uint32_t)A + i] + (uint64_t)NL[idx] + (with_step ? (uint64_t)D16[idx] : 0ull);
-        else return N[idx];
+        } else {
+            return N[idx];
+        }
     };
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
     const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * (nthr + 2u) * 2u)),
@@ -667,9 +705,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         return (two >> ((off & 3u) * 8u)) & row_mask;
     };
     auto flag_nan = [](uint32_t f) -> bool { return (f & QF_NAN) || (f & (QF_PINF | QF_NINF)) == (QF_PINF | QF_NINF); };
-    // f64 image of entry idx (exact: |raw| <= 2^51)
-    auto val = [&](uint32_t idx, int64_t raw) -> double {
-        if constexpr (SPEC) return q_val(raw, QF8[idx] & QF_MASK);
+    // f64 image of an entry's word (fixed point: exact, |raw| <= 2^51)
+    auto val = [&](int64_t raw) -> double {
+        if constexpr (FQ) return as_f64((uint64_t)raw);
         else return q_val(raw);
     };
     // raw rows of state s: table 0 and (double policy) table 1, read once per use
@@ -701,7 +739,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // Agent::get_action = selector(Policy::predict(s)) against the step snapshot;
     // UCB counter increments are applied by the caller after a barrier.
     // single-table Q-learning: the selection's argmax and the TD target's max are
-    // of the same row s2, so both come from one pass (argmax_max_i64) computed for
+    // of the same row s2, so both come from one pass (argmax_max_*) computed for
     // the whole wave before the selection; `pre` is that argmax (-1: none)
     constexpr bool FUSE_MAX = RLAMD_FUSE_MAX && !UCB && P == 1 && ALGO == RL_ALGO_QLEARNING;
     auto select = [&](uint32_t s, const int64_t (&ra)[A], const int64_t (&rb)[A], int32_t pre = -1) -> uint32_t {
@@ -711,39 +749,46 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (explore) explore = uniform01(L.rng) < L.eps;
             if (explore) return uniform_action<A>(L.rng);
             if constexpr (FUSE_MAX) return (uint32_t)pre;
-            int64_t v[A];                           // argmax of predict() on exact raw sums
+            if constexpr (FQ) {                     // argmax of predict(): (a + b) / 2.0 (double_tabular_policy.rs:31-39)
+                double v[A];
 #pragma unroll
-            for (int i = 0; i < A; ++i) v[i] = P == 2 ? ra[i] + rb[i] : ra[i];
-            return argmax_i64<A>(v);
+                for (int i = 0; i < A; ++i) v[i] = P == 2 ? (as_f64(ra[i]) + as_f64(rb[i])) / 2.0 : as_f64(ra[i]);
+                return argmax<A>(v);
+            } else {                                // argmax on exact raw values (single table)
+                return argmax_i64<A>(ra);
+            }
         } else {                                    // upper_confidence_bound.rs:29-42
             double u[A], v[A];
             uint64_t n[A];
             const double lnt = ESU ? lnt_cur(T[0]) : rl_log((double)T[0]);
 #pragma unroll
             for (int i = 0; i < A; ++i) {
-                v[i] = val(qi(0, s, i), ra[i]);
-                if constexpr (P == 2) v[i] = (v[i] + val(qi(1, s, i), rb[i])) / 2.0;
+                v[i] = val(ra[i]);
+                if constexpr (P == 2) v[i] = (v[i] + val(rb[i])) / 2.0;
                 n[i] = ucount(s, (uint32_t)i, false);
             }
             uint32_t need = ucb_known<A>(v, n, p.ucb_c, lnt, u);
             // argmax (utils.rs:1-11) is decided without the unknown (finite) values
-            // when u[0] is NaN (it sticks) or some known u is +inf (the first wins)
+            // when u[0] is NaN (it sticks) or some known u is +inf (the first wins);
+            // unknown values are finite only while |c| < 2^1020 (ucb_known)
+            const bool c_fin = __builtin_fabs(p.ucb_c) < 0x1p1020;
             bool decided = (need & 1u) == 0u && u[0] != u[0];
 #pragma unroll
-            for (int i = 0; i < A; ++i) decided = decided || (((need >> i) & 1u) == 0u && u[i] == __builtin_inf());
+            for (int i = 0; i < A; ++i)
+                decided = decided || (c_fin && ((need >> i) & 1u) == 0u && u[i] == __builtin_inf());
             if (need && !decided) ucb_fill<A>(v, n, p.ucb_c, lnt, need, u);
             return argmax<A>(u);
         }
     };
-    // add n contributions summing to `sum` to entry idx.  Sweep form (the table
-    // fits the block, PSA <= nthr): thread i settles entry i every step, so the
-    // counter add needs no return value.  Owner form: the step's first
+    // fixed point: add n contributions summing to `sum` to entry idx.  Sweep form
+    // (the table fits the block, PSA <= nthr): thread i settles entry i every step,
+    // so the counter add needs no return value.  Owner form: the step's first
     // contributor (old count 0) settles the entry.
     const bool sweep = SWEEP == 1 || PSAL <= nthr;   // SWEEP == 1: the host checked PSA <= block
     // PACKC: one LDS atomic per contribution — SUM[idx] holds sum * 2^11 + count
     // (KParams::pack_ok: the host proved |sum| * 2^11 + 2047 < 2^63)
-    constexpr bool PACKC = PACK && !SPEC && !TRACES;
-    auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n, uint32_t fl) -> bool {
+    constexpr bool PACKC = PACK && !FQ;
+    auto contribute = [&](uint32_t idx, int64_t sum, uint32_t n) -> bool {
         if constexpr (PACKC) {
             const unsigned long long v = (unsigned long long)(sum * 2048) + n;
             if (sweep) { atomicAdd(&SUM[idx], v); return false; }
@@ -754,24 +799,38 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if (sweep) atomicAdd(&CNT[idx >> 1], n << sh);
         else first = ((atomicAdd(&CNT[idx >> 1], n << sh) >> sh) & 0xffffu) == 0u;
         if (sum) atomicAdd(&SUM[idx], (unsigned long long)sum);
-        if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
         return first;
     };
-    // owner: Q[idx] += mean of the step's contributions (clamped), clear
-    // accumulators; returns whether the clamp engaged (counted by the caller with
-    // a wave ballot after reconvergence: no branch, no VGPR)
-    auto settle = [&](uint32_t idx) -> bool {
+    // fixed point owner: Q[idx] += mean of the step's contributions (proven in
+    // range: no clamp), clear accumulators
+    auto settle = [&](uint32_t idx) {
         const int64_t packed = (int64_t)SUM[idx];
         const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[idx];
         const int64_t sum = PACKC ? (packed >> 11) : packed;
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
-        bool hit = false;
-        if constexpr (HITS) Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp(sum, rc), hit);
-        else Q[idx] = Q[idx] + (unsigned long long)mean_delta_rcp(sum, rc);   // proven in range: no clamp
+        Q[idx] = Q[idx] + (unsigned long long)mean_delta_rcp(sum, rc);
         SUM[idx] = 0ull;
         if constexpr (!PACKC) CNT16[idx] = 0;
-        if constexpr (SPEC) fold_flags(QF8, idx);
-        return hit;
+    };
+    // f64 owner: the entry moves by the mean of the step's contributions on their
+    // grid (or by the IEEE result of its non-finite ones), NaN canonical
+    auto settle_fq = [&](uint32_t idx) {
+        const uint32_t w = W[idx], n = w & 0xffffu;
+        if (n == 0u) return;                       // sweep form: untouched this step
+        const uint32_t f = ((uint32_t)SFL8[idx] >> SFL_SH) & QF_MASK;
+        double dl;
+        if (f) {
+            dl = nf_value(f);
+        } else {
+            const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;
+            dl = __builtin_ldexp((double)(int64_t)SUM[idx] * rc, fq_grid((w >> 16) - 1u));
+        }
+        const double q = canon_nan(as_f64(Q[idx]) + dl);
+        Q[idx] = f64_bits(q);
+        SUM[idx] = 0ull;
+        W[idx] = 0u;
+        if constexpr (SPEC) QF8[idx] = (uint8_t)value_flags(q);
+        else if (f) SFL8[idx] = 0;
     };
     // traces: every action of a visited state receives a contribution
     // (elegibility_traces_agent.rs:82-96), so the A entries of an LDS row share
@@ -783,25 +842,36 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     auto qi_row = [&](uint32_t tbl, uint32_t row, uint32_t a) -> uint32_t {
         return LDS_AM ? tbl * SAL + a * SL + row : tbl * SAL + row * (uint32_t)A + a;
     };
-    auto settle_row = [&](uint32_t rid) -> uint32_t {   // rid = tbl*SL + LDS row; returns clamp hits
+    // f64 traces: one grid per group step, 2^e with e from the step's largest finite
+    // |td| and the trace bound (oracle rlref.c fq_step_combine)
+    auto contrib_tr = [&](uint32_t idx, double d, int e) {
+        if (__builtin_isfinite(d)) {
+            const int64_t raw = fq_raw(d, e);
+            if (raw) atomicAdd(&SUM[idx], (unsigned long long)raw);
+        } else {
+            atomicOr(&SFLW[idx >> 2], (nf_flag(d) << SFL_SH) << ((idx & 3u) * 8u));
+        }
+    };
+    auto settle_row = [&](uint32_t rid, int e) {   // rid = tbl*SL + LDS row
         const uint32_t n = CNTR[rid];
+        if (n == 0u) return;
         const double rc = n < lay.nrcp ? RCP[n] : 1.0 / (double)n;
         const uint32_t tbl = rid / SL, row = rid - tbl * SL;
-        uint32_t hits = 0;
 #pragma unroll
         for (int b = 0; b < A; ++b) {
             const uint32_t idx = qi_row(tbl, row, (uint32_t)b);
-            bool hit;
-            Q[idx] = (unsigned long long)q_clamp((int64_t)Q[idx] + mean_delta_rcp((int64_t)SUM[idx], rc), hit);
-            hits += hit ? 1u : 0u;
+            const uint32_t f = ((uint32_t)SFL8[idx] >> SFL_SH) & QF_MASK;
+            const double dl = f ? nf_value(f) : __builtin_ldexp((double)(int64_t)SUM[idx] * rc, e);
+            const double q = canon_nan(as_f64(Q[idx]) + dl);
+            Q[idx] = f64_bits(q);
             SUM[idx] = 0ull;
-            if constexpr (SPEC) fold_flags(QF8, idx);
+            if constexpr (SPEC) QF8[idx] = (uint8_t)value_flags(q);
+            else if (f) SFL8[idx] = 0;
         }
         CNTR[rid] = 0u;
-        return hits;
     };
     // wave-level per-launch counters (scalar registers: ballot popcounts)
-    uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0, c_clamp = 0, c_sat = 0;
+    uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
     unsigned long long *const RSUM = &ACC[4];
 
     for (uint32_t k = 0; k < p.K; ++k) {
@@ -826,7 +896,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     const uint32_t s0 = E::reset(L.z, L.rng, tabs);
                     L.ready = true;
                     load_rows(s0, ra2, rb2);
-                    L.a = select(s0, ra2, rb2, FUSE_MAX ? (int32_t)argmax_i64<A>(ra2) : -1);
+                    int32_t pre = -1;
+                    if constexpr (FUSE_MAX) {
+                        if constexpr (FQ) {
+                            double v[A], m;
+#pragma unroll
+                            for (int i = 0; i < A; ++i) v[i] = as_f64(ra2[i]);
+                            pre = (int32_t)argmax_max_f64<A>(v, m);
+                        } else {
+                            pre = (int32_t)argmax_i64<A>(ra2);
+                        }
+                    }
+                    L.a = select(s0, ra2, rb2, pre);
                     L.s = s0;
                     L.need_reset = false;
                     L.epi_reward = 0.0;
@@ -873,36 +954,46 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
         }
         int64_t rmax = 0;                   // FUSE_MAX: utils::max of row s2 (the Q-learning target)
+        double rmaxd = 0.0;
         int32_t rarg = -1;
         if constexpr (FUSE_MAX) {
-            rarg = (int32_t)argmax_max_i64<A>(ra2, rmax);
-            // pin both here (empty asm): left alone, the compiler sinks the index into
-            // the exploit branch and the max into the TD branch, redoing the compares
-            if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmax));
+            if constexpr (FQ) {
+                double v[A];
+#pragma unroll
+                for (int i = 0; i < A; ++i) v[i] = as_f64(ra2[i]);
+                rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
+                if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
+            } else {
+                rarg = (int32_t)argmax_max_i64<A>(ra2, rmax);
+                // pin both here (empty asm): left alone, the compiler sinks the index into
+                // the exploit branch and the max into the TD branch, redoing the compares
+                if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmax));
+            }
         }
-#if RLAMD_EXP & 4   // timing experiment: greedy selection, no RNG (results differ)
-        if (alive) { int64_t v[A]; for (int i = 0; i < A; ++i) v[i] = ra2[i]; a2 = argmax_i64<A>(v); }
-#else
         if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2, rarg);
-#endif
-        uint32_t d_own = 0xffffffffu;   // SPEC: the D entry this lane settles at step end
+        uint32_t d_own = 0xffffffffu;   // SPEC: the step-count entry this lane folds at step end
         if constexpr (SPEC) {
-            // the step's increments go to D / T[1], apart from what this step's
-            // selections read (NL, T[0]), so no barrier separates the two; expected
-            // SARSA's probabilities read n + D and T[0] + T[1] after the barrier
+            // the step's increments go to the step counts / T[1], apart from what this
+            // step's selections read (launch counts, T[0]), so no barrier separates the
+            // two; expected SARSA's probabilities read both after the arrival below
             if (alive) {
-                const uint32_t idx = qi(0, s2, a2), sh = (idx & 1u) * 16u;
-                if (((atomicAdd(&D32[idx >> 1], 1u << sh) >> sh) & 0xffffu) == 0u) d_own = idx;
+                const uint32_t idx = qi(0, s2, a2);
+                if (p.ucb_pack) {
+                    if ((atomicAdd(&NL[idx], 1u) & 0xffffu) == 0u) d_own = idx;
+                } else {
+                    const uint32_t sh = (idx & 1u) * 16u;
+                    if (((atomicAdd(&D32[idx >> 1], 1u << sh) >> sh) & 0xffffu) == 0u) d_own = idx;
+                }
             }
             const uint32_t c = (uint32_t)__popcll(__ballot(alive));
             if ((tid & 63u) == 0 && c) atomicAdd(&T[1], (unsigned long long)c);
             // one-sided barrier: every wave announces that its increments are in
             // (ARR counts arrivals over the launch); only a wave with a lane whose
-            // target row is finite reads n + D / T, so only such a wave waits for all
-            // arrivals of this step.  No wave passes the end-of-step barrier before
+            // target row is finite reads the counts / T, so only such a wave waits for
+            // all arrivals of this step.  No wave passes the end-of-step barrier before
             // arriving, so ARR >= (k+1) * waves means exactly that.  In the all-NaN
-            // regime no wave waits.  What the others go on to do meanwhile (SUM/CNT
-            // contributions, pending QF bits) is invisible to the step's readers.
+            // regime no wave waits.  What the others go on to do meanwhile (their
+            // contributions) is invisible to the step's readers.
             uint32_t *ARR = (uint32_t *)(T + 2);
             __threadfence_block();
             if ((tid & 63u) == 0) atomicAdd(ARR, 1u);
@@ -933,15 +1024,26 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             for (int i = 0; i < A; ++i) rv[i] = vt ? rb2[i] : ra2[i];
             double fq;
             if constexpr (ALGO == RL_ALGO_QLEARNING && !SPEC) {
-                fq = q_val(FUSE_MAX ? rmax : max_i64<A>(rv));   // utils::max on exact images
+                if constexpr (FQ) {
+                    if constexpr (FUSE_MAX) {
+                        fq = rmaxd;
+                    } else {
+                        double v[A];
+#pragma unroll
+                        for (int i = 0; i < A; ++i) v[i] = as_f64(rv[i]);
+                        fq = vmax<A>(v);                   // utils::max
+                    }
+                } else {
+                    fq = q_val(FUSE_MAX ? rmax : max_i64<A>(rv));   // utils::max on exact images
+                }
             } else if constexpr (ALGO == RL_ALGO_SARSA && !SPEC) {
-                fq = q_val(pick<A>(rv, a2));
+                fq = val(pick<A>(rv, a2));
             } else if (SPEC && tgt_nf) {
                 fq = __builtin_nan("");
             } else {
                 double q2[A], pr[A];
 #pragma unroll
-                for (int i = 0; i < A; ++i) q2[i] = val(qi(vt, s2, i), rv[i]);
+                for (int i = 0; i < A; ++i) q2[i] = val(rv[i]);
                 if constexpr (!UCB) {
                     eps_probs<A>(L.eps, q2, pr);
                 } else {                                   // upper_confidence_bound.rs:48-63
@@ -973,42 +1075,56 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 td = __builtin_nan("");                    // r + gamma * NaN - q
             } else {
                 const uint32_t qidx = qi(vt, L.s, L.a);
-                const double qa = val(qidx, (int64_t)Q[qidx]);
+                const double qa = val((int64_t)Q[qidx]);
                 td = r + p.gamma * fq - qa;
             }
         }
         if constexpr (!TRACES) {
             const uint32_t idx = qi(ut, L.s, L.a);
-            bool owner = false, sat = false;
-            if (train) {
-                uint32_t fl = 0;
-                int64_t dq;
-                if constexpr (SPEC) dq = q_fix(p.lr * td, fl, sat);
-                else if constexpr (HITS) dq = q_fix_finite(p.lr * td, sat);
-                else dq = q_fix_inrange(p.lr * td);
-#if RLAMD_EXP & 2   // timing experiment: no LDS atomics (results differ)
-                owner = dq == 12345;
-#else
-                owner = contribute(idx, dq, 1u, fl);
-#endif
+            if constexpr (FQ) {
+                // pass 1: the step's largest code per entry (+1: 0 marks an untouched
+                // entry) and the kinds of its non-finite contributions; the first
+                // contributor owns the entry's settle
+                double d = 0.0;
+                bool fin = true, owner = false;
+                if (train) {
+                    d = p.lr * td;                         // tabular_policy.rs:36 (lr * td)
+                    fin = __builtin_isfinite(d);
+                    owner = atomicMax(&W[idx], (fin ? f64_code(d) + 1u : 1u) << 16) == 0u;
+                    if (!fin) atomicOr(&SFLW[idx >> 2], (nf_flag(d) << SFL_SH) << ((idx & 3u) * 8u));
+                }
+                __syncthreads();   // every code in
+                // pass 2: the contribution on its entry's grid, and the count
+                if (train) {
+                    if (fin) {
+                        const int64_t raw = fq_raw(d, fq_grid((W[idx] >> 16) - 1u));
+                        if (raw) atomicAdd(&SUM[idx], (unsigned long long)raw);
+                    }
+                    atomicAdd(&W[idx], 1u);
+                }
+                __syncthreads();   // all contributions in, all Q reads done
+                if (sweep) { if (tid < PSAL) settle_fq(tid); }
+                else if (owner) settle_fq(idx);
+            } else {
+                bool owner = false;
+                if (train) owner = contribute(idx, q_fix_inrange(p.lr * td), 1u);
+                __syncthreads();   // all contributions in, all Q reads done
+                if (sweep) { if (tid < PSAL) settle(tid); }
+                else if (owner) settle(idx);
             }
-            if constexpr (HITS) c_sat += (uint32_t)__popcll(__ballot(sat));
-#if !(RLAMD_EXP & 16)   // timing experiment: no contributions barrier (results differ)
-            __syncthreads();   // all contributions in, all Q reads done
-#endif
-            bool hit = false;
-#if RLAMD_EXP & 1   // timing experiment: no settle sweep (results differ)
-            if (sweep) { if (tid < PSA && CNT16[tid] == 77) hit = settle(tid); }
-#else
-            if (sweep) { if (tid < PSAL) hit = settle(tid); }
-#endif
-            else if (owner) hit = settle(idx);
-            if constexpr (HITS) c_clamp += (uint32_t)__popcll(__ballot(hit));
         } else {
             // accumulating trace: E[s][a] += 1, then for every visited (o, b):
             // Q[o][b] += lr*(td*E[o][b]); E[o][b] *= gamma*lambda; E cleared on
-            // termination (elegibility_traces_agent.rs:75-101).  Every lane walks its
-            // own visited set; slot j of all lanes is one coalesced row.
+            // termination (elegibility_traces_agent.rs:75-101).
+            // The group step's grid: 2^e from the largest finite |td| of its lanes
+            int e_tr;
+            {
+                const uint32_t c = (train && __builtin_isfinite(td)) ? f64_code(td) : 0u;
+                const uint32_t wm = wave_max_u32(c);
+                if ((tid & 63u) == 0 && wm) atomicMax(GCODE, wm);
+                __syncthreads();
+                e_tr = fq_grid(GCODE[0]) + p.trace_k;
+            }
             if constexpr (PAIRS && RLAMD_COOP_SWEEP) {
                 uint32_t hid = 0xffffu;      // PBITS: the visited pair whose E += 1 the sweep applies
                 if constexpr (PBITS) {
@@ -1129,20 +1245,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                                 if (rsweep) atomicAdd(&CNTR[rid], 1u);
                                 else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
                             }
-                            bool sat;
-                            const int64_t d = q_fix_finite(p.lr * (td_o * ev), sat);
-                            if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
-                            if (d) atomicAdd(&SUM[qi(ut_o, o, b)], (unsigned long long)d);
+                            contrib_tr(qi(ut_o, o, b), p.lr * (td_o * ev), e_tr);
                             const double en = ev * p.gl;
                             if (in_lds) pc.TRE[pc.ixe_t(j, col)] = en;
                             else p.trace[pslot(p, j, lanev[u])] = en;
                         }
                     }
-                }
-                if (train && term) {
-                    pair_clear(p, pc, lane, tcnt);
-#pragma unroll
-                    for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
                 }
             } else if constexpr (PAIRS) {
                 if (train) pair_visit<A>(p, pc, lane, L.s, L.a, tcnt);
@@ -1154,55 +1262,79 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         if (rsweep) atomicAdd(&CNTR[rid], 1u);
                         else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
                     }
-                    bool sat;
-                    const int64_t d = q_fix_finite(p.lr * (td * ev), sat);
-                    if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
-                    if (d) atomicAdd(&SUM[qi(ut, o, b)], (unsigned long long)d);
+                    contrib_tr(qi(ut, o, b), p.lr * (td * ev), e_tr);
                 });
-                if (train && term) pair_clear(p, pc, lane, tcnt);
             } else {
-            if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
-            const uint32_t nv = train ? tcnt : 0u;
-            trace_states += nv;
-            trace_sweep<A>(p, lane, nv,
-              [&](uint32_t o) {                            // once per visited state: its row count
-                const uint32_t rid = ut * SL + lrow(o);
-                if (rsweep) atomicAdd(&CNTR[rid], 1u);
-                else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
-              },
-              [&](uint32_t o, uint32_t b, double ev) {
-                uint32_t fl = 0;
-                int64_t d;
-                bool sat;
-                if constexpr (SPEC) d = q_fix(p.lr * (td * ev), fl, sat);
-                else d = q_fix_finite(p.lr * (td * ev), sat);
-                if (sat) atomicAdd(&ACC[ACC_SAT], 1ull);
-                const uint32_t idx = qi(ut, o, b);
-                if (d) atomicAdd(&SUM[idx], (unsigned long long)d);
-                if constexpr (SPEC) { if (fl) atomicOr(&QF[idx >> 2], (fl << QF_PENDING) << ((idx & 3u) * 8u)); }
-            });
+                if (train) trace_visit<A>(p, lane, L.s, L.a, tcnt);
+                const uint32_t nv = train ? tcnt : 0u;
+                trace_states += nv;
+                trace_sweep<A>(p, lane, nv,
+                  [&](uint32_t o) {                            // once per visited state: its row count
+                    const uint32_t rid = ut * SL + lrow(o);
+                    if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                    else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+                  },
+                  [&](uint32_t o, uint32_t b, double ev) { contrib_tr(qi(ut, o, b), p.lr * (td * ev), e_tr); });
+            }
+            if constexpr (PAIRS) {
+                // a non-finite td also moves the never-taken actions of every visited
+                // state, whose E is 0: lr * (td * 0) is NaN (elegibility_traces_agent.rs:
+                // 86-96 sweeps whole rows); the pair lists hold only taken actions
+                if (train && !__builtin_isfinite(td)) {
+                    const double dn = p.lr * (td * 0.0);
+                    auto id_at = [&](uint32_t j) -> uint32_t {
+                        return j < pc.cap ? (uint32_t)pc.TRI[pc.ixi(j)] : (uint32_t)p.tlist[pslot(p, j, lane)];
+                    };
+                    for (uint32_t j = 0; j < tcnt; ++j) {
+                        const uint32_t w = id_at(j);
+                        if (!(w & 0x8000u)) continue;
+                        const uint32_t o = (w & 0x7fffu) / (uint32_t)A;
+                        uint32_t taken = 0;
+                        if constexpr (PBITS) {
+                            taken = (pbits_word((o * (uint32_t)A) >> 5) >> ((o * (uint32_t)A) & 31u)) & 0xfu;
+                        } else {
+                            for (uint32_t i = 0; i < tcnt; ++i) {
+                                const uint32_t x = (id_at(i) & 0x7fffu) - o * (uint32_t)A;
+                                if (x < (uint32_t)A) taken |= 1u << x;
+                            }
+                        }
+                        for (uint32_t b = 0; b < (uint32_t)A; ++b)
+                            if (!((taken >> b) & 1u)) contrib_tr(qi(ut, o, b), dn, e_tr);
+                    }
+                }
+                if (train && term) {
+                    pair_clear(p, pc, lane, tcnt);
+                    if constexpr (PBITS) {
+#pragma unroll
+                        for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
+                    }
+                }
             }
             if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
+            if (tid == 0) GCODE[0] = 0u;                  // read by every thread before the sweep
             if (rsweep) {
-                const uint32_t h = tid < (uint32_t)P * SL ? settle_row(tid) : 0u;
-                if (h) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)h);
+                if (tid < (uint32_t)P * SL) settle_row(tid, e_tr);
             } else {
                 const uint32_t n_touched = LISTN[0];
-                uint32_t h = 0;
-                for (uint32_t i = tid; i < n_touched; i += nthr) h += settle_row(LIST[i]);
-                if (h) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)h);
+                for (uint32_t i = tid; i < n_touched; i += nthr) settle_row(LIST[i], e_tr);
                 __syncthreads();
                 if (tid == 0) LISTN[0] = 0u;
             }
         }
         if constexpr (SPEC) {                     // fold the step's counter increments
-            if (d_own != 0xffffffffu) { NL[d_own] += (uint32_t)D16[d_own]; D16[d_own] = 0; }
+            if (d_own != 0xffffffffu) {
+                if (p.ucb_pack) {
+                    const uint32_t w = NL[d_own];
+                    NL[d_own] = ((w >> 16) + (w & 0xffffu)) << 16;
+                } else {
+                    NL[d_own] += (uint32_t)D16[d_own];
+                    D16[d_own] = 0;
+                }
+            }
             if (tid == 0) { T[0] += T[1]; T[1] = 0ull; }
         }
-#if !(RLAMD_EXP & 8)   // timing experiment: no end-of-step barrier (results differ)
         __syncthreads();   // Q_{t+1} complete before the next step's reads
-#endif
         bool tr = false, ev = false;
         if (doS) {
             if (train) {
@@ -1214,10 +1346,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
             if (INSTR && p.rec) write_record(p, k, lane, fused ? 3u : 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
             after_step(p, L, s2, a2, r, term, tr, ev);
-            // !HITS: the host also proved |episode reward| * 2^16 < 2^51 (delta_bound), so
-            // rint is the magic add
-            if (tr) atomicAdd(RSUM, (unsigned long long)(HITS ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
-                                                               : rint_i64_small(L.epi_reward * 65536.0)));
+            // fixed point: the host also proved |episode reward| * 2^16 < 2^51
+            // (delta_bound), so rint is the magic add
+            if (tr) atomicAdd(RSUM, (unsigned long long)(FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
+                                                             : rint_i64_small(L.epi_reward * 65536.0)));
             if (INSTR && p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         } else if (doR) {
             L.s = s2;
@@ -1247,8 +1379,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if (c_eval) atomicAdd(&ACC[1], (unsigned long long)c_eval);
             if (c_tep) atomicAdd(&ACC[2], (unsigned long long)c_tep);
             if (c_eep) atomicAdd(&ACC[3], (unsigned long long)c_eep);
-            if (c_clamp) atomicAdd(&ACC[ACC_CLAMP], (unsigned long long)c_clamp);
-            if (c_sat) atomicAdd(&ACC[ACC_SAT], (unsigned long long)c_sat);
             if (c_done) atomicAdd(&ACC[5], (unsigned long long)c_done);
         }
         if constexpr (TRACES) {
@@ -1258,43 +1388,41 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         flush_block(p, ACC);
     }
 
-    // ---------------- emit this group's ΔQ (and ΔN, Δt, new flags) for the merge
-    // delta layout: [PSA sums][PSA group counts][SA dN][1 dt][3*PSA flag counts],
-    // into replica blockIdx % n_rep (folded by k_fold_replicas)
+    // ---------------- emit this group's changes for the merge.  Fixed point:
+    // ΔQ and group counts into replica blockIdx % n_rep of the SUM words ([PSA
+    // sums][PSA group counts][SA dN][1 dt], folded by k_fold_replicas); f64: the
+    // group's Q values into its slot (k_fq_merge_a / _b take the mean).
     int64_t *const dl = p.delta_rep + (uint64_t)(blockIdx.x % p.n_rep) * p.delta_words;
     __syncthreads();
-    for (uint32_t j = tid; j < PSAL; j += nthr) {
-        const uint32_t i = dense_of(j);
-        const int64_t d = (int64_t)(Q[j] - (unsigned long long)p.q_base[i]);
-        if (d) {
-            atomicAdd((unsigned long long *)&dl[i], (unsigned long long)d);
-            atomicAdd((unsigned long long *)&dl[PSA + i], 1ull);
+    if constexpr (FQ) {
+        uint64_t *const slot = p.qslot + (uint64_t)blockIdx.x * PSAL;
+        for (uint32_t j = tid; j < PSAL; j += nthr) slot[j] = Q[j];
+    } else {
+        for (uint32_t j = tid; j < PSAL; j += nthr) {
+            const uint32_t i = dense_of(j);
+            const int64_t d = (int64_t)(Q[j] - (unsigned long long)p.q_base[i]);
+            if (d) {
+                atomicAdd((unsigned long long *)&dl[i], (unsigned long long)d);
+                atomicAdd((unsigned long long *)&dl[PSA + i], 1ull);
+            }
         }
     }
     if constexpr (UCB) {
         for (uint32_t i = tid; i < SA; i += nthr) {
-            const int64_t d = SPEC ? (int64_t)NL[i] : (int64_t)(N[lds_of(i)] - (unsigned long long)p.n_base[i]);
+            const int64_t d = SPEC ? (int64_t)(p.ucb_pack ? (NL[i] >> 16) : NL[i])
+                                   : (int64_t)(N[lds_of(i)] - (unsigned long long)p.n_base[i]);
             if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + i], (unsigned long long)d);
         }
         if (tid == 0) {
             const int64_t d = (int64_t)(T[0] - p.t_base[0]);
             if (d) atomicAdd((unsigned long long *)&dl[2 * PSA + SA], (unsigned long long)d);
         }
-        if constexpr (SPEC) {
-            int64_t *fc = dl + 2 * PSA + SA + 1;
-            for (uint32_t i = tid; i < PSA; i += nthr) {
-                const uint32_t nf = QF8[lds_of(i)] & ~p.qf_base[i];
-                if (nf & QF_NAN) atomicAdd((unsigned long long *)&fc[i], 1ull);
-                if (nf & QF_PINF) atomicAdd((unsigned long long *)&fc[PSA + i], 1ull);
-                if (nf & QF_NINF) atomicAdd((unsigned long long *)&fc[2 * PSA + i], 1ull);
-            }
-        }
     }
 }
 
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, bool FQ>
 __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, INSTR>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, INSTR, FQ>(p);
 }
 // Eligibility traces on the small tables (FrozenLake, CliffWalking: the pair
 // bitmap) in groups of <= 256 lanes, at most 2 groups per CU (cfg 4: 2^17 lanes in
@@ -1303,55 +1431,53 @@ __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
 // of the 128-VGPR bound's scratch spills
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_train_shared_w(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, true>(p);
 }
 template <int ENV, int AGENT, int POLICY>
 constexpr bool use_w() {
     return RLAMD_TRACES_W && AGENT == RL_AGENT_TRACES && POLICY != RL_POLICY_NEURAL &&
            (ENV == RL_ENV_CLIFF_WALKING || ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED);
 }
+// the shared kernel for the agent's representation (nullptr: the fixed point
+// cannot be proven for this variant, so the host never asks for it)
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
+const void *shared_kernel(const KParams &p) {
+    if (p.fq) return (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, true>;
+    if constexpr (fix_possible<AGENT, POLICY, SEL, ALGO>())
+        return (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, false>;
+    return nullptr;
+}
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
 // learner groups whose LDS footprint allows 8 waves: one-step tabular
-// FrozenLake / CliffWalking and one-step eps-greedy Blackjack.  The other
-// variants would spill for no occupancy.
-// It counts clamp hits / delta saturations only for UCB + expected SARSA (SURVEY
-// F7: unbounded bootstrap weights); every other configuration runs it only when
-// the host proved both counts 0 (KParams::hits_zero), else k_train_shared.
-template <int SEL, int ALGO>
-constexpr bool o8_counts_hits() { return SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA; }
-// MODE 0: counts clamp hits / saturations (and clamps); 1: the host proved the
-// range (no counting, no clamps); 2: as 1, with packed (sum, count) contributions
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
+// FrozenLake / CliffWalking in the fixed point (proven range), and one-step
+// eps-greedy Blackjack (single or double table) in the fixed point or in f64.
+// The other variants would spill for no occupancy.
+// MODE 1: fixed point; 2: fixed point with packed (sum, count) contributions; 3: f64
 #ifndef RLAMD_O8_WAVES
-#define RLAMD_O8_WAVES 8   // waves per SIMD the o8 kernels are compiled for (timing experiments: 6)
+#define RLAMD_O8_WAVES 8   // waves per SIMD the o8 kernels are compiled for
 #endif
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RLAMD_O8_WAVES, RLAMD_O8_WAVES))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, SLIP, SWEEP, MODE == 0, MODE == 2, RS>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, MODE == 3, SLIP, SWEEP, MODE == 2, RS>(p);
 }
 // the reset-and-step schedule is compiled into the 8-wave kernels only where it
 // is the measured better schedule (Blackjack, eps-greedy); elsewhere it runs on
 // k_train_shared, and the 8-wave kernels carry no trace of it
 template <int ENV, int SEL>
 constexpr bool o8_has_reset_step() { return ENV == RL_ENV_BLACKJACK && SEL == RL_SEL_EPS_GREEDY; }
-// the 8-wave kernel for (SLIP, SWEEP), packed contributions when the host proved them exact
-// nullptr: no 8-wave kernel for this case (unproven range outside Blackjack: the
-// caller takes k_train_shared, which counts)
+// the 8-wave kernel for (SLIP, SWEEP) and the agent's representation; nullptr: none
+// (the caller takes k_train_shared)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int RS>
 const void *o8_kernel_rs(const KParams &p) {
-    if constexpr (o8_counts_hits<SEL, ALGO>()) {
-        return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 0, RS>;
-    } else {
-        if (p.hits_zero)
-            return p.pack_ok ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 2, RS>
-                             : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1, RS>;
-        // Blackjack double Q (cfg 5) is not range-provable (the double policy's update
-        // is not a contraction of the written table), so its 8-wave kernel counts
-        if constexpr (ENV == RL_ENV_BLACKJACK)
-            return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 0, RS>;
+    if (p.fq) {
+        if constexpr (ENV == RL_ENV_BLACKJACK) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 3, RS>;
         return nullptr;
     }
+    if constexpr (fix_possible<AGENT, POLICY, SEL, ALGO>())
+        return p.pack_ok ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 2, RS>
+                         : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1, RS>;
+    return nullptr;
 }
-// nullptr: no 8-wave kernel for this schedule (the caller takes k_train_shared)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
 const void *o8_kernel(const KParams &p) {
     if constexpr (o8_has_reset_step<ENV, SEL>()) {
@@ -1364,7 +1490,7 @@ const void *o8_kernel(const KParams &p) {
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 constexpr bool use_o8() {
     return ((ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_CLIFF_WALKING) && AGENT == RL_AGENT_ONE_STEP &&
-            POLICY == RL_POLICY_TABULAR) ||
+            POLICY == RL_POLICY_TABULAR && !(SEL == RL_SEL_UCB && ALGO == RL_ALGO_EXPECTED_SARSA)) ||
            // Blackjack eps-greedy (compact rows: <= 35 KiB per group of 512, four groups
            // per CU): 67 VGPRs at the default bound left it at 3 groups per CU, i.e. a
            // second, one-third-full round of workgroups for cfg 5's 1024 groups per GPU
@@ -1602,14 +1728,13 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int PRIV>
 hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hipStream_t stream, int *occ) {
     const bool instr = p.rec != nullptr || p.elog != nullptr;
-    const void *k;
+    const void *k = nullptr;
     if constexpr (PRIV) {
         k = (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>;
     } else if (instr) {
-        k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, true>;
+        k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, true>(p);
     } else {
         if constexpr (use_o8<ENV, AGENT, POLICY, SEL, ALGO>()) {
-          {
             // the map's slippery flag (FrozenLake) and the settle form (every entry
             // owned by one thread when P*S*A <= block size) as compile-time constants
             const bool sw = p.P * p.S * p.A <= block.x;
@@ -1622,16 +1747,13 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
                 k = sw ? o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, 1>(p)
                        : o8_kernel<ENV, AGENT, POLICY, SEL, ALGO, -1, -1>(p);
             }
-          }
-          if (!k) k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
         } else if constexpr (use_w<ENV, AGENT, POLICY>()) {
             // 256 CUs: <= 512 groups keeps the grid at <= 2 groups (2 waves per SIMD) per CU
-            k = (block.x <= 256 && grid.x <= 512) ? (const void *)k_train_shared_w<ENV, AGENT, POLICY, SEL, ALGO>
-                                                  : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
-        } else {
-            k = (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, false>;
+            if (p.fq && block.x <= 256 && grid.x <= 512) k = (const void *)k_train_shared_w<ENV, AGENT, POLICY, SEL, ALGO>;
         }
+        if (!k) k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, false>(p);
     }
+    if (!k) return hipErrorInvalidValue;   // the fixed point for a variant it cannot prove
     if (smem > 64 * 1024) {   // gfx950: a workgroup may use up to the CU's 160 KiB of LDS
         const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;

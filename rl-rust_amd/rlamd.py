@@ -72,6 +72,8 @@ RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
                          ("term", "u1"), ("mode", "u1"), ("kind", "u1"), ("pad", "u1", (3,)),
                          ("r", "<f8"), ("td", "<f8")])
 KIND_IDLE, KIND_RESET, KIND_STEP = 0, 1, 2
+QREPR = {0: "fixed40", 1: "f64", 2: "private"}     # rl.h rl_q_repr
+QMODE = {"auto": 0, "f64": 1}                       # rl.h rl_q_mode
 EPISODE_DTYPE = np.dtype([("lane", "<u4"), ("length", "<u4"), ("seq", "<u4"), ("mode", "u1"),
                           ("pad", "u1", (3,)), ("reward", "<f8")])
 
@@ -81,6 +83,7 @@ _V = C.c_void_p
 SIGNATURES = {
     "rl_last_error": (C.c_char_p, []),
     "rl_abi_version": (C.c_int, []),
+    "rl_build_info": (C.c_char_p, []),
     "rl_device_count": (C.c_int, [_P(C.c_int)]),
     "rl_blackjack_obs_id": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32]),
     "rl_obs_to_reference": (C.c_uint64, [C.c_int32, C.c_uint32]),
@@ -104,6 +107,8 @@ SIGNATURES = {
     "rl_agent_get_q": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_set_q": (C.c_int, [_V, _V, C.c_size_t]),
     "rl_agent_get_q_raw": (C.c_int, [_V, _V, C.c_size_t]),
+    "rl_agent_q_repr": (C.c_int, [_V, _P(C.c_int32)]),
+    "rl_agent_set_q_mode": (C.c_int, [_V, C.c_int32]),
     "rl_agent_get_ucb": (C.c_int, [_V, _V, C.c_size_t, _V, C.c_size_t]),
     "rl_agent_set_ucb": (C.c_int, [_V, _V, C.c_size_t, _V, C.c_size_t]),
     "rl_agent_get_epsilon": (C.c_int, [_V, _V, C.c_size_t]),
@@ -116,8 +121,11 @@ SIGNATURES = {
     "rl_agent_dims": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint32), _P(C.c_uint32)]),
     "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
     "rl_agent_delta_words": (C.c_int, [_V, _P(C.c_uint64)]),
+    "rl_agent_delta_max_words": (C.c_int, [_V, _P(C.c_uint64)]),
     "rl_agent_set_delta_buffer": (C.c_int, [_V, _V, C.c_uint64]),
+    "rl_agent_set_merge_groups": (C.c_int, [_V, C.c_uint64]),
     "rl_agent_launch_train": (C.c_int, [_V]),
+    "rl_agent_launch_fold": (C.c_int, [_V]),
     "rl_agent_launch_apply": (C.c_int, [_V]),
     "rl_agent_set_stream": (C.c_int, [_V, _V]),
     "rl_agent_occupancy": (C.c_int, [_V, _P(C.c_uint32), _P(C.c_uint64), _P(C.c_uint32)]),
@@ -334,10 +342,20 @@ class Agent:
         check(lib().rl_agent_set_q(self.h, q.ctypes.data, q.size))
 
     def q_raw(self):
+        """raw words of the shared Q: fixed-point integers or f64 bits (q_repr())"""
         n = self.P * self.S * self.A
         out = np.zeros(n, np.int64)
         check(lib().rl_agent_get_q_raw(self.h, out.ctypes.data, n))
         return out.reshape(self.P, self.S, self.A)
+
+    def q_repr(self):
+        r = C.c_int32()
+        check(lib().rl_agent_q_repr(self.h, C.byref(r)))
+        return QREPR[r.value]
+
+    def set_q_mode(self, mode):
+        """'auto' (the 2^-40 fixed point where its range is proven) or 'f64'"""
+        check(lib().rl_agent_set_q_mode(self.h, QMODE[mode]))
 
     def ucb(self):
         if self.private:
@@ -415,11 +433,24 @@ class Agent:
         check(lib().rl_agent_lane_state(self.h, core.ctypes.data, aux.ctypes.data, self.L))
         return core, aux
 
-    # ---- multi-GPU merge as an external collective
+    # ---- multi-GPU merge as an external collective:
+    # launch_train -> all-reduce MAX of the first delta_max_words() words ->
+    # launch_fold -> all-reduce SUM of the rest -> launch_apply
     def delta_words(self):
         n = C.c_uint64()
         check(lib().rl_agent_delta_words(self.h, C.byref(n)))
         return n.value
+
+    def delta_max_words(self):
+        n = C.c_uint64()
+        check(lib().rl_agent_delta_max_words(self.h, C.byref(n)))
+        return n.value
+
+    def set_merge_groups(self, total_groups):
+        check(lib().rl_agent_set_merge_groups(self.h, total_groups))
+
+    def launch_fold(self):
+        check(lib().rl_agent_launch_fold(self.h))
 
     def set_delta_buffer(self, ptr, n_words):
         check(lib().rl_agent_set_delta_buffer(self.h, C.c_void_p(ptr), n_words))
@@ -436,7 +467,7 @@ class Agent:
         check(lib().rl_agent_set_comm(self.h, comm.h if comm is not None else None))
 
     def sync(self):
-        """the merge after launch_train(): RCCL all-reduce of the delta, then apply"""
+        """the merge after launch_train(): RCCL all-reduces (MAX, fold, SUM), then apply"""
         check(lib().rl_agent_sync(self.h))
 
     def set_stream(self, stream_ptr):

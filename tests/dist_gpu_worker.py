@@ -2,7 +2,8 @@
 torch.distributed.run; gloo, every rank on the box's one GPU).
 
 Each rank owns the contiguous global lanes [rank*L, (rank+1)*L) and runs the
-bench.py step: rl_agent_launch_train -> all_reduce(int64 delta) ->
+bench.py step: rl_agent_launch_train -> all_reduce(MAX of the leading merge
+words) -> rl_agent_launch_fold -> all_reduce(SUM of the rest) ->
 rl_agent_launch_apply.  Rank 0 then runs ONE agent holding all world*L lanes
 for the same number of launches (rl_agent_run: the in-process merge) and
 writes whether raw Q, UCB counters and t are bit-identical, plus the step
@@ -31,11 +32,19 @@ def main():
     p = rlamd.default_params(n_lanes=L, lane_offset=rank * L, **case)
     a = rlamd.Agent(p)
     delta = torch.zeros(a.delta_words(), dtype=torch.int64, device="cuda:0")
+    mw = a.delta_max_words()
     a.set_delta_buffer(delta.data_ptr(), delta.numel())
+    groups = (L + case["group_size"] - 1) // case["group_size"]
+    a.set_merge_groups(world * groups)          # the f64 merge grid counts every rank's groups
+    repr_rank = a.q_repr()
     for _ in range(n_launch):
         a.launch_train()
         torch.cuda.synchronize()
-        dist.all_reduce(delta)
+        dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
+        torch.cuda.synchronize()
+        a.launch_fold()
+        torch.cuda.synchronize()
+        dist.all_reduce(delta[mw:])
         torch.cuda.synchronize()
         a.launch_apply()
     a.synchronize()
@@ -57,6 +66,7 @@ def main():
                                                np.nan_to_num(qf1).view(np.uint64))),
                "q_nonfinite": int(np.count_nonzero(~np.isfinite(qf))),
                "q_nonzero": int(np.count_nonzero(q)),
+               "q_repr": [repr_rank, one.q_repr()],
                "steps_ranks": int(steps.item()), "steps_one": int(one.stats()["train_steps"])}
         if ucb is not None:
             u1 = one.ucb()

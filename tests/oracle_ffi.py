@@ -45,6 +45,9 @@ RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
                          ("term", "u1"), ("mode", "u1"), ("kind", "u1"), ("pad", "u1", (3,)),
                          ("r", "<f8"), ("td", "<f8")])
 KIND_IDLE, KIND_RESET, KIND_STEP, KIND_RESET_STEP = 0, 1, 2, 3
+# shared-Q representation (oracle/rlref.h): reported / requested
+QREPR = {0: "fixed40", 1: "f64", 2: "private"}
+QMODE = {"auto": 0, "f64": 1, "f64_seq": 2}
 assert RECORD_DTYPE.itemsize == 32
 
 
@@ -160,6 +163,15 @@ def lib():
         L.rlo_batch_delta_words.argtypes = [C.c_void_p]
         L.rlo_batch_launch_groups.argtypes = [C.c_void_p, C.c_void_p]
         L.rlo_batch_apply_delta.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_delta_max_words.restype = C.c_uint64
+        L.rlo_batch_delta_max_words.argtypes = [C.c_void_p]
+        L.rlo_batch_fold.argtypes = [C.c_void_p, C.c_void_p]
+        L.rlo_batch_set_q_mode.argtypes = [C.c_void_p, C.c_int]
+        L.rlo_batch_q_repr.restype = C.c_int
+        L.rlo_batch_q_repr.argtypes = [C.c_void_p]
+        L.rlo_batch_set_merge_groups.argtypes = [C.c_void_p, C.c_uint64]
+        L.rlo_trace_grid_k.restype = C.c_int
+        L.rlo_trace_grid_k.argtypes = [C.c_double, C.c_double, C.c_double, C.c_uint32, C.c_int32]
         L.rlo_batch_n_records.restype = C.c_uint64
         L.rlo_batch_n_records.argtypes = [C.c_void_p]
         L.rlo_batch_stats.argtypes = [C.c_void_p, C.c_void_p]
@@ -349,7 +361,8 @@ class Faithful:
 
 
 class Batch:
-    """The batched schedule the GPU implements (fixed-point Q)."""
+    """The batched schedule the GPU implements (shared Q as 2^-40 fixed point where
+    the range proof holds, else f64 with exponent-grid sums; rlref.c section 2)."""
 
     def __init__(self, p):
         self.p = p
@@ -443,13 +456,33 @@ class Batch:
         lib().rlo_batch_take_records(self.h, out.ctypes.data, n)
         return out.reshape(-1, self.L)
 
+    def set_q_mode(self, mode):
+        """'auto' (fixed point where proven), 'f64', or 'f64_seq' (oracle only: f64
+        with sequential lane-order / group-order sums, the drift reference)"""
+        lib().rlo_batch_set_q_mode(self.h, QMODE[mode])
+
+    def q_repr(self):
+        return QREPR[lib().rlo_batch_q_repr(self.h)]
+
+    def set_merge_groups(self, total_groups):
+        lib().rlo_batch_set_merge_groups(self.h, total_groups)
+
     def delta_words(self):
+        """merge buffer words: delta_max_words() MAX words, then the SUM words"""
         return lib().rlo_batch_delta_words(self.h)
+
+    def delta_max_words(self):
+        return lib().rlo_batch_delta_max_words(self.h)
 
     def launch_groups(self, delta):
         """run local groups for K steps, adding their merge delta into `delta` (int64)"""
         assert delta.dtype == np.int64 and delta.flags.c_contiguous
         lib().rlo_batch_launch_groups(self.h, delta.ctypes.data)
+
+    def fold(self, delta):
+        """second merge phase (after the MAX all-reduce of the first words)"""
+        assert delta.dtype == np.int64 and delta.flags.c_contiguous
+        lib().rlo_batch_fold(self.h, delta.ctypes.data)
 
     def apply_delta(self, delta):
         lib().rlo_batch_apply_delta(self.h, np.ascontiguousarray(delta, np.int64).ctypes.data)

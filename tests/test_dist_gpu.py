@@ -2,8 +2,10 @@
 
 The driver runs bench.py at N = 2/4/8 over RCCL (librlamd's rl_comm) on a whole node; these tests
 exercise the same per-rank code path on real hardware:
-  - the per-rank merge (launch_train -> all_reduce(int64 delta) -> launch_apply)
-    gives raw Q / UCB counters bit-identical to one process holding every lane;
+  - the per-rank merge (launch_train -> all_reduce MAX -> launch_fold ->
+    all_reduce SUM -> launch_apply) gives raw Q / UCB counters bit-identical to
+    one process holding every lane, in both Q representations (the fixed point
+    for FrozenLake Q-learning, f64 for the rest);
   - `python -m torch.distributed.run ... bench.py --gpus 2` prints one valid
     JSON line on rank 0 (whole-job value, max-over-ranks wall time).
 Both run as child processes launched before this process touches the GPU.
@@ -55,6 +57,7 @@ def test_two_rank_device_merge_equals_one_process(tmp_path, name):
     assert res["steps_ranks"] == res["steps_one"] > 0, res
     assert res["q_nonzero"] + res["q_nonfinite"] > 0, res   # UCB+E-SARSA: all-NaN/inf is legal (F7)
     assert res["q_equal"] and res["qf_equal"], res
+    assert res["q_repr"][0] == res["q_repr"][1] == ("fixed40" if name == "fl8x8-qlearning" else "f64"), res
     if "ucb_equal" in res:
         assert res["ucb_equal"], res
 

@@ -1,10 +1,10 @@
-"""GPU parity for the counters and arming rules added in round 2.
+"""GPU parity for the counters and arming rules.
 
 - UCB visit counters are u64 (the reference keeps u128,
   src/action_selection/upper_confidence_bound.rs:11-12): seeded just below
   2^32, they must cross it without wrapping, bit-exact vs the oracle.
-- The fixed-point Q range events are counted (rl_stats::q_clamp_hits /
-  delta_saturations) identically on the device and in the oracle.
+- Tables outside the fixed point's proven range are f64 (rl.h rl_q_repr): the
+  hyper-parameters that used to clamp run unclamped, bit-exact vs the oracle.
 - train() / evaluate() leave every lane in TRAIN at an episode start with an
   empty trace set (elegibility_traces_agent.rs:98-100), so run() keeps training.
 """
@@ -78,28 +78,31 @@ def test_set_ucb_rejects_t_zero(rl):
                                   dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=64),
                                   dict(env="taxi", selector="ucb", algo="qlearning", group_size=100)],
                          ids=["cw-q", "cw-traces", "taxi-ucb"])
-def test_clamp_and_saturation_counters(rl, oracle, case):
-    """Q pinned at the -2048 edge (gamma 1, q_default -2047.5: every -1 step
-    pushes past it) and lr 30 (a -100 cliff step saturates the per-lane delta):
-    both counters nonzero and equal to the oracle's, Q bit-exact."""
+def test_out_of_range_tables_are_f64(rl, oracle, case):
+    """gamma 1, q_default -2047.5, lr 30: no range proof, so the table is f64 —
+    values leave [-2048, 2048] unclamped, bit-exact vs the oracle (ABI v3 clamped
+    and counted these; v4 has no clamp, the counters stay 0)."""
     p = rl.default_params(n_lanes=500, sync_every=16, gamma=1.0, lr=30.0, q_default=-2047.5, **case)
     dev, ref = rl.Agent(p), oracle.Batch(p)
+    assert dev.q_repr() == ref.q_repr() == "f64"
     dev.run(4)
     ref.run(4)
     assert np.array_equal(dev.q_raw(), ref.q_raw())
-    st, rs = dev.stats(), ref.stats()
-    assert st["q_clamp_hits"] == int(rs[8]) and st["q_clamp_hits"] > 0
-    assert st["delta_saturations"] == int(rs[9])
-    if case["env"] == "cliff_walking":
-        assert st["delta_saturations"] > 0
+    q = dev.q()
+    assert (q[np.isfinite(q)] < -2048.0).any()
+    st = dev.stats()
+    assert st["q_clamp_hits"] == 0 and st["delta_saturations"] == 0
     _assert_stats_equal(dev, ref)
 
 
-def test_default_configs_never_clamp(rl):
-    """At the reference CLI's hyper-parameters the fixed-point range is never hit."""
-    for kw in (dict(env="frozen_lake", map8x8=1), dict(env="cliff_walking", agent="traces", algo="sarsa"),
-               dict(env="blackjack", policy="double")):
+def test_default_configs_representation(rl):
+    """At the reference CLI's hyper-parameters: FrozenLake Q-learning is proven
+    (fixed point), traces and the double policy are f64; no counter moves."""
+    for kw, want in ((dict(env="frozen_lake", map8x8=1), "fixed40"),
+                     (dict(env="cliff_walking", agent="traces", algo="sarsa"), "f64"),
+                     (dict(env="blackjack", policy="double"), "f64")):
         a = rl.Agent(rl.default_params(n_lanes=4096, group_size=256, **kw))
+        assert a.q_repr() == want, kw
         a.run(4)
         st = a.stats()
         assert st["q_clamp_hits"] == 0 and st["delta_saturations"] == 0, (kw, st)
@@ -145,11 +148,11 @@ def test_train_then_run_keeps_training(rl, oracle, G):
 
 
 @pytest.mark.parametrize("reset_step", [False, True], ids=["one-action", "reset-and-step"])
-def test_double_policy_clamps_are_counted_and_exact(rl, oracle, reset_step):
+def test_double_policy_follows_f64_range(rl, oracle, reset_step):
     """The double policy writes one table with the TD error of the other
-    (double_tabular_policy.rs:31-67), so A - B grows by (1 + lr) per update pair and
-    long runs reach the +-2048 fixed-point clamp (cfg 5 does at bench length): no
-    range proof applies, the 8-wave kernel counts and clamps, bit-exact vs the oracle."""
+    (double_tabular_policy.rs:31-67), so A - B grows by (1 + lr) per update pair:
+    the values leave the old fixed-point range (|Q| <= 2048) within the run and the
+    f64 tables follow them, bit-exact vs the oracle, with no clamp."""
     p = rl.default_params(env="blackjack", policy="double", algo="qlearning", n_lanes=4096, group_size=512,
                           sync_every=64)
     dev, ref = rl.Agent(p), oracle.Batch(p)
@@ -158,6 +161,8 @@ def test_double_policy_clamps_are_counted_and_exact(rl, oracle, reset_step):
     dev.run(40)
     ref.run(40)
     assert np.array_equal(dev.q_raw(), ref.q_raw())
-    st, rs = dev.stats(), ref.stats()
-    assert st["q_clamp_hits"] == int(rs[8]) and st["q_clamp_hits"] > 0, (st, rs[8])
+    q = dev.q()
+    assert dev.q_repr() == "f64" and np.nanmax(np.abs(q)) > 2048.0, np.nanmax(np.abs(q))
+    st = dev.stats()
+    assert st["q_clamp_hits"] == 0
     _assert_stats_equal(dev, ref)

@@ -75,31 +75,116 @@ def test_shared_mode_stays_in_range(oracle):
     assert q.min() >= 0.0 and q.max() <= 1.0 + 1e-12 and q.max() > 0.0
 
 
-def test_set_q_fixed_point_and_blackjack_terminal_rows(oracle):
-    """rlo_batch_set_q stores the values as the merge base does (fixed point
-    2^-40, clamp at 2^51, NaN/inf as flags), and Blackjack terminal rows
-    (player > 21 or dealer card > 10) are never written by training."""
+def test_set_q_representations_and_blackjack_terminal_rows(oracle):
+    """rlo_batch_set_q keeps the values as given: the double policy has no range
+    proof, so the table is f64 (5000, NaN, inf held exactly, NaN canonical); and
+    Blackjack terminal rows (player > 21 or dealer card > 10) are never written
+    by training."""
     p = oracle.default_params(env="blackjack", policy="double", algo="qlearning", n_lanes=512, group_size=128,
                               sync_every=16)
     b = oracle.Batch(p)
+    assert b.q_repr() == "f64"
     P, S, A = b.P, b.S, b.A
     q = np.random.default_rng(4).uniform(-2.0, 2.0, (P, S, A))
     q[0, 5, 1] = np.nan
     q[1, 7, 0] = np.inf
-    q[0, 9, 0] = 5000.0                      # clamped to 2^51 * 2^-40 = 2048
+    q[0, 9, 0] = 5000.0                      # no clamp: f64 keeps it
     b.set_q(q.reshape(-1))
     raw = b.q_raw()
-    fin = np.isfinite(q) & (np.abs(q) < 2048)
-    assert np.array_equal(raw[fin], np.rint(q[fin] * 2.0**40).astype(np.int64))
-    assert raw[0, 9, 0] == 2**51
+    fin = np.isfinite(q)
+    assert np.array_equal(raw[fin].view(np.float64), q[fin])
+    assert raw[0, 5, 1] == 0x7FF8000000000000
     qq = b.q()
-    assert np.isnan(qq[0, 5, 1]) and qq[1, 7, 0] == np.inf
+    assert np.isnan(qq[0, 5, 1]) and qq[1, 7, 0] == np.inf and qq[0, 9, 0] == 5000.0
     s = np.arange(S)
     term = ~((s >> 6 <= 21) & ((s >> 1) & 31 <= 10))
     before = raw[:, term, :].copy()
     b.run(6)
     assert np.array_equal(b.q_raw()[:, term, :], before)
     assert not np.array_equal(b.q_raw()[:, ~term, :], raw[:, ~term, :])
+
+
+@pytest.mark.parametrize("kw,want", [
+    (dict(env="frozen_lake", map8x8=1, algo="qlearning"), "fixed40"),
+    (dict(env="taxi", algo="expected_sarsa"), "fixed40"),
+    (dict(env="cliff_walking", selector="ucb", algo="sarsa"), "fixed40"),
+    (dict(env="blackjack", policy="double", algo="qlearning"), "f64"),
+    (dict(env="cliff_walking", agent="traces", algo="sarsa"), "f64"),
+    (dict(env="taxi", selector="ucb", algo="expected_sarsa"), "f64"),
+    (dict(env="frozen_lake", algo="qlearning", gamma=1.0), "f64"),
+], ids=["fl-q", "taxi-es", "cw-ucb-sarsa", "bj-double", "cw-traces", "taxi-ucb-es", "gamma1"])
+def test_representation_follows_the_range_proof(oracle, kw, want):
+    """The fixed point only where the proof holds (one-step, single table,
+    contracting bootstrap: rlref.c o_delta_bound), f64 everywhere else."""
+    b = oracle.Batch(oracle.default_params(n_lanes=64, group_size=32, **kw))
+    assert b.q_repr() == want
+
+
+def test_representation_changes(oracle):
+    """set_q with values the fixed point cannot hold exactly -> f64; a selector /
+    algorithm change that breaks the proof moves a fixed-point table to f64 exactly
+    (the proof follows the table's state); set_q_mode switches both ways."""
+    p = oracle.default_params(env="frozen_lake", map8x8=1, algo="qlearning", n_lanes=256, group_size=64, sync_every=8)
+    b = oracle.Batch(p)
+    assert b.q_repr() == "fixed40"
+    b.run(3)
+    q0 = b.q()
+    b.set_q_mode("f64")
+    assert b.q_repr() == "f64" and np.array_equal(b.q(), q0)
+    b.set_q_mode("auto")
+    assert b.q_repr() == "fixed40" and np.array_equal(b.q(), q0)
+    b.set_selector("ucb")
+    b.set_algo("expected_sarsa")                  # UCB + expected SARSA: no proof
+    assert b.q_repr() == "f64" and np.array_equal(b.q(), q0)
+    b.set_q(np.full(b.P * b.S * b.A, 0.1))      # 0.1 is not a multiple of 2^-40
+    assert b.q_repr() == "f64"
+
+
+def test_f64_one_lane_is_the_reference_loop(oracle):
+    """With one lane every step has one contribution per entry, added exactly
+    (Q += lr * td, tabular_policy.rs:35-38 / double_tabular_policy.rs:50-57), and the
+    merge of one group is its value: the shared f64 schedule IS the reference loop,
+    bit for bit, including the double policy's growth to +-inf / NaN."""
+    for kw in (dict(env="blackjack", policy="double", algo="qlearning"),
+               dict(env="taxi", selector="ucb", algo="expected_sarsa"),
+               dict(env="cliff_walking", policy="double", selector="ucb", algo="sarsa")):
+        n = 2000
+        p = oracle.default_params(n_episodes_for_decay=n, n_lanes=1, group_size=2, sync_every=37, **kw)
+        b = oracle.Batch(p)
+        b.set_q_mode("f64")
+        b.train_episodes(n, n // 4)
+        f = oracle.Faithful(p)
+        f.train(n, n // 4)
+        assert _eq_nan(b.q(), f.q()), kw
+
+
+def test_f64_double_policy_grows_past_the_old_clamp(oracle):
+    """cfg 5's update (double_tabular_policy.rs:50-57) is not a contraction: the
+    values leave the fixed point's [-2048, 2048] within a few hundred steps of the
+    bench geometry, and the f64 table follows them (no clamp, no saturation)."""
+    p = oracle.default_params(env="blackjack", policy="double", algo="qlearning", n_lanes=2048, group_size=512,
+                              sync_every=64)
+    b = oracle.Batch(p)
+    b.set_reset_step(True)
+    b.run(12)
+    q = b.q()
+    assert b.q_repr() == "f64" and np.nanmax(np.abs(q)) > 2048.0
+    st = b.stats()
+    assert st[8] == 0 and st[9] == 0
+
+
+def test_f64_sequential_variant_drift_is_small(oracle):
+    """The exponent-grid sum vs f64 sums in lane / group order (rlref.c
+    RLO_QMODE_F64_SEQ): same draws, same mean rule; the two only differ by
+    rounding, bounded relative to the values over a short horizon."""
+    kw = dict(env="cliff_walking", agent="traces", algo="sarsa", n_lanes=512, group_size=128, sync_every=16)
+    a = oracle.Batch(oracle.default_params(**kw))
+    s = oracle.Batch(oracle.default_params(**kw))
+    s.set_q_mode("f64_seq")
+    a.run(4)
+    s.run(4)
+    qa, qs = a.q(), s.q()
+    assert np.isfinite(qa).all() and np.abs(qa - qs).max() < 1e-9 * max(1.0, np.abs(qa).max())
 
 
 def test_expected_sarsa_ucb_nan_is_sticky(oracle):
@@ -131,24 +216,32 @@ def _rank_main(rank, world, port, p, n_launch, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     L = p["n_lanes"] // world
     b = O.Batch(dict(p, n_lanes=L, lane_offset=rank * L))
+    b.set_merge_groups(world * ((L + p["group_size"] - 1) // p["group_size"]))
+    mw = b.delta_max_words()
     for _ in range(n_launch):
         d = np.zeros(b.delta_words(), np.int64)
         b.launch_groups(d)
-        t = torch.from_numpy(d)
-        dist.all_reduce(t)                     # the RCCL all-reduce of bench.py, on gloo
+        t = torch.from_numpy(d)                # the RCCL all-reduces of bench.py, on gloo
+        dist.all_reduce(t[:mw], op=dist.ReduceOp.MAX)
+        b.fold(d)
+        dist.all_reduce(t[mw:])
         b.apply_delta(t.numpy())
     out_q.put((rank, b.q_raw().tobytes(), b.ucb()[0].tobytes(), b.ucb()[1]))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("case", [dict(env="frozen_lake", map8x8=1, algo="qlearning"),
-                                  dict(env="taxi", selector="ucb", algo="sarsa")],
-                         ids=["fl8x8-q", "taxi-ucb-sarsa"])
+                                  dict(env="taxi", selector="ucb", algo="sarsa"),
+                                  dict(env="blackjack", policy="double", algo="qlearning"),
+                                  dict(env="cliff_walking", agent="traces", algo="sarsa"),
+                                  dict(env="taxi", selector="ucb", algo="expected_sarsa")],
+                         ids=["fl8x8-q", "taxi-ucb-sarsa", "bj-double-f64", "cw-traces-f64", "taxi-ucb-es-f64"])
 def test_two_rank_merge_equals_one_process(oracle, case):
     """world_size-2 gloo: each rank holds half the lanes (contiguous global lane
-    ids), all-reduces the int64 merge delta, applies it.  Q and UCB counters
-    must be bit-identical to one process holding every lane (GPU-count
-    independence of the N>1 bench path)."""
+    ids), all-reduces the merge buffer (MAX of the f64 grid codes, fold, SUM of the
+    rest), applies it.  Q and UCB counters must be bit-identical to one process
+    holding every lane (GPU-count independence of the N>1 bench path), in both
+    Q representations."""
     import torch.multiprocessing as mp
     p = oracle.default_params(n_lanes=512, group_size=64, sync_every=16, **case)
     n_launch = 5
