@@ -108,17 +108,17 @@ def cpu_baseline(args):
     """SURVEY §8(d) CPU reference timing, on this host's cores, bounded samples.
 
     value  — "ref_faithful" (oracle/ref_faithful.c): the reference's single-env
-             loop with its own data structures (FxHashMap Q, per-step TD Vec push,
-             ChaCha12 draws, eval interleave every n/10 episodes), the bench's
-             workload (FrozenLake 8x8 Q-learning eps-greedy) at the CLI defaults
-             (n_episodes 1e5, src/bin/frozen_lake.rs:35-73), 1 core; whole training
+             loop with its own data structures (FxHashMap Q / double-Q maps / trace
+             map / UCB counters, per-step TD Vec push, ChaCha12 draws, eval
+             interleave every n/10 episodes, Blackjack's fxhash observation ids),
+             for THIS workload's env / agent / policy / selector / algorithm at the
+             CLI defaults (n_episodes 1e5, src/bin/*.rs), 1 core; whole training
              runs repeated (train -> reset, as the bins' sweep) until the sample
              lasts about `cpu_seconds`.
     multi_core — the same, one independent env per thread, on every core the
              process may use (len(os.sched_getaffinity(0)), recorded in `cores`).
     cfg1   — SURVEY cfg 1: FrozenLake 4x4 one-step Q-learning eps-greedy, 1 core.
     ref_dense — the oracle's dense-array restatement of the same loop, 1 core.
-    Non-FrozenLake workloads report ref_dense only (ref_faithful covers FrozenLake).
     Every number is a C restatement of the reference loop, not the Rust binary
     (no Rust toolchain here: SURVEY §8(c))."""
     odir = os.path.join(ROOT, "oracle", "_build")
@@ -132,9 +132,10 @@ def cpu_baseline(args):
     algok = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}[args.algo]
     n, eval_at = 100000, 10000          # the bins: train(env, n_episodes, n_episodes / 10)
 
-    def run_rf(map8, reps, threads):
-        out = subprocess.run([rf, str(map8), str(args.slippery), str(selk), str(algok), str(n), str(eval_at),
-                              str(reps), str(threads)], check=True, capture_output=True, text=True).stdout
+    def run_rf(env, map8, agent, pol, sel, algo, reps, threads):
+        out = subprocess.run([rf, str(env), str(map8), str(args.slippery), str(agent), str(pol), str(sel), str(algo),
+                              str(n), str(eval_at), str(reps), str(threads)],
+                             check=True, capture_output=True, text=True).stdout
         return json.loads(out)
 
     def run_dense(reps, threads):
@@ -158,24 +159,21 @@ def cpu_baseline(args):
     # every core this process may run on (the box's share: sched_getaffinity, not
     # os.cpu_count(), which counts the whole machine)
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    fl = args.env == "frozen_lake" and args.agent == "one_step" and args.policy == "tabular"
-    desc = (f"{args.env}{' 8x8' if args.map8x8 else ''}{' slippery' if args.slippery else ''} "
-            f"{args.agent} {args.algo} {args.selector}")
-    if fl:
-        reps, r = sized(lambda k: run_rf(args.map8x8, k, 1), args.cpu_seconds)
-        res = line("port", f"ref_faithful (oracle/ref_faithful.c: FxHashMap Q, ChaCha12, Vec histories) {desc}",
-                   reps, r, 1)
-        reps_m, m = sized(lambda k: run_rf(args.map8x8, k, threads), args.cpu_seconds / 2)
-        res["multi_core"] = line("port", f"{threads} independent ref_faithful envs", reps_m, m, threads)
-        reps1, c1 = sized(lambda k: run_rf(0, k, 1), args.cpu_seconds / 4)
-        res["cfg1"] = line("port", "SURVEY cfg 1: ref_faithful FrozenLake 4x4 one-step Q-learning eps-greedy",
-                           reps1, c1, 1)
-    repd, d = sized(lambda k: run_dense(k, 1), args.cpu_seconds / (4 if fl else 1))
-    dl = line("port", f"ref_dense (oracle/rlref.c rlo_faithful: dense-array Q) {desc}", repd, d, 1)
-    if not fl:
-        return dl
-    res["ref_dense"] = dl
-    res["host_threads_available"] = os.cpu_count()
+    desc = (f"{args.env}{' 8x8' if args.map8x8 and args.env == 'frozen_lake' else ''}"
+            f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} {args.algo} {args.selector}")
+    mine = (envk, args.map8x8, agentk, polk, selk, algok)
+    reps, r = sized(lambda k: run_rf(*mine, k, 1), args.cpu_seconds)
+    res = line("port", f"ref_faithful (oracle/ref_faithful.c: FxHashMap tables, ChaCha12, Vec histories) {desc}",
+               reps, r, 1)
+    reps_m, m = sized(lambda k: run_rf(*mine, k, threads), args.cpu_seconds / 2)
+    res["multi_core"] = line("port", f"{threads} independent ref_faithful envs (len(os.sched_getaffinity(0)))",
+                             reps_m, m, threads)
+    reps1, c1 = sized(lambda k: run_rf(0, 0, 0, 0, 0, 1, k, 1), args.cpu_seconds / 4)
+    res["cfg1"] = line("port", "SURVEY cfg 1: ref_faithful FrozenLake 4x4 one-step Q-learning eps-greedy",
+                       reps1, c1, 1)
+    repd, d = sized(lambda k: run_dense(k, 1), args.cpu_seconds / 4)
+    res["ref_dense"] = line("port", f"ref_dense (oracle/rlref.c rlo_faithful: dense-array Q) {desc}", repd, d, 1)
+    res["host_threads_machine"] = os.cpu_count()
     return res
 
 

@@ -52,9 +52,9 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 //   sum  int64 [P][S][A]   this step's summed contributions per entry (integers:
 //                          the fixed point's units, or the f64 entry's grid)
 //   cnt  fixed point: u16 [P][S][A] contributions per entry (u32-word atomics);
-//        f64 one-step: u32 [P][S][A] = max code + 1 << 16 | count; traces: u32
-//        per (table, row) contribution counts
-//   sfl  u8  [P][S][A]     f64: kinds of this step's non-finite contributions
+//        f64 one-step: u32 [P][S][A] = kinds of non-finite contributions << 28 |
+//        (max code + 1) << 16 | count; traces: u32 per (table, row) counts
+//   sfl  u8  [P][S][A]     f64 traces: kinds of this step's non-finite contributions
 //                          (UCB + expected SARSA: bits 4-6 of qf instead)
 //   qf   u8  [P][S][A]     UCB + expected SARSA: visible NaN/+-inf kinds of the entries
 //   n/t  UCB counters (u64 [S][A], u64 t);  list u16 touched rows + count (traces)
@@ -83,7 +83,7 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.q = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.sum = off; off += shared_q ? align16(PSA * 8u) : 0u;
     l.cnt = off; off += shared_q ? align16((fq && !traces) ? PSA * 4u : ((PSA + 1u) / 2u) * 4u) : 0u;
-    l.sfl = off; off += (shared_q && fq && ucb != 2) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
+    l.sfl = off; off += (shared_q && fq && traces && ucb != 2) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
     l.qf = off; off += (shared_q && ucb == 2) ? align16(((PSA + 3u) / 4u) * 4u) : 0u;
     l.n = off;
     l.nd = off + align16(SA * 4u);
@@ -546,8 +546,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // fixed point: two u16 counters per word
     uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
-    uint32_t *W = (uint32_t *)(smem + lay.cnt);          // f64 one-step: max code + 1 << 16 | count
-    // f64: kinds of the step's non-finite contributions (own bytes; QF's bits 4-6 for SPEC)
+    uint32_t *W = (uint32_t *)(smem + lay.cnt);          // f64 one-step: kinds << 28 | max code + 1 << 16 | count
+    // f64 traces: kinds of the step's non-finite contributions (own bytes; QF's bits 4-6 for SPEC)
     uint32_t *SFLW = (uint32_t *)(smem + (SPEC ? lay.qf : lay.sfl));
     uint8_t *SFL8 = (uint8_t *)(smem + (SPEC ? lay.qf : lay.sfl));
     constexpr uint32_t SFL_SH = SPEC ? QF_PENDING : 0u;
@@ -600,7 +600,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     } else {
         for (uint32_t i = tid; i < (PSAL + 1u) / 2u; i += nthr) CNT[i] = 0u;
     }
-    if constexpr (FQ && !SPEC)
+    if constexpr (FQ && TRACES && !SPEC)
         for (uint32_t i = tid; i < (PSAL + 3u) / 4u; i += nthr) SFLW[i] = 0u;
     if constexpr (TRACES) { if (tid == 0) LISTN[0] = 0u; }
     if constexpr (UCB) {
@@ -815,22 +815,21 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // f64 owner: the entry moves by the mean of the step's contributions on their
     // grid (or by the IEEE result of its non-finite ones), NaN canonical
     auto settle_fq = [&](uint32_t idx) {
-        const uint32_t w = W[idx], n = w & 0xffffu;
+        const uint32_t w = W[idx], n = w & 0xfffu;
         if (n == 0u) return;                       // sweep form: untouched this step
-        const uint32_t f = ((uint32_t)SFL8[idx] >> SFL_SH) & QF_MASK;
+        const uint32_t f = w >> 28;
         double dl;
         if (f) {
             dl = nf_value(f);
         } else {
             const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;
-            dl = __builtin_ldexp((double)(int64_t)SUM[idx] * rc, fq_grid((w >> 16) - 1u));
+            dl = __builtin_ldexp((double)(int64_t)SUM[idx] * rc, fq_grid(((w >> 16) & 0xfffu) - 1u));
         }
         const double q = canon_nan(as_f64(Q[idx]) + dl);
         Q[idx] = f64_bits(q);
         SUM[idx] = 0ull;
         W[idx] = 0u;
         if constexpr (SPEC) QF8[idx] = (uint8_t)value_flags(q);
-        else if (f) SFL8[idx] = 0;
     };
     // traces: every action of a visited state receives a contribution
     // (elegibility_traces_agent.rs:82-96), so the A entries of an LDS row share
@@ -1083,21 +1082,24 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             const uint32_t idx = qi(ut, L.s, L.a);
             if constexpr (FQ) {
                 // pass 1: the step's largest code per entry (+1: 0 marks an untouched
-                // entry) and the kinds of its non-finite contributions; the first
-                // contributor owns the entry's settle
+                // entry) or the kinds of its non-finite contributions, in the top bits
+                // (a max after them leaves them: the code no longer matters then); the
+                // first contributor owns the entry's settle
                 double d = 0.0;
                 bool fin = true, owner = false;
                 if (train) {
                     d = p.lr * td;                         // tabular_policy.rs:36 (lr * td)
                     fin = __builtin_isfinite(d);
-                    owner = atomicMax(&W[idx], (fin ? f64_code(d) + 1u : 1u) << 16) == 0u;
-                    if (!fin) atomicOr(&SFLW[idx >> 2], (nf_flag(d) << SFL_SH) << ((idx & 3u) * 8u));
+                    const uint32_t old = fin ? atomicMax(&W[idx], (f64_code(d) + 1u) << 16)
+                                             : atomicOr(&W[idx], nf_flag(d) << 28);
+                    owner = old == 0u;
                 }
                 __syncthreads();   // every code in
                 // pass 2: the contribution on its entry's grid, and the count
                 if (train) {
-                    if (fin) {
-                        const int64_t raw = fq_raw(d, fq_grid((W[idx] >> 16) - 1u));
+                    const uint32_t w = W[idx];
+                    if (fin && (w >> 28) == 0u) {
+                        const int64_t raw = fq_raw(d, fq_grid(((w >> 16) & 0xfffu) - 1u));
                         if (raw) atomicAdd(&SUM[idx], (unsigned long long)raw);
                     }
                     atomicAdd(&W[idx], 1u);

@@ -1,0 +1,91 @@
+"""Bench-length golden fixtures: the oracle's batched
+schedule at bench.py's exact configurations for as many launches as one default
+bench run makes (1 warm-up + 64 timed = 65 launches of K = 64 synchronous steps),
+so the device is pinned over the whole benchmarked window — past the point where
+cfg 5's double tables leave the old fixed-point range (|Q| > 2048) and where
+cfg 3's UCB + expected SARSA table is mostly NaN.
+
+Stored per case: raw Q words (f64 bits, NaN canonical), the representation, the
+NaN / +-inf counts and the largest finite |Q|, stats, UCB counters, a SHA-256 of
+every lane's epsilon.  Also stored, as a MEASUREMENT (not a parity bar): the
+same run with every step / merge sum formed sequentially in lane / group order
+in f64 (the oracle's RLO_QMODE_F64_SEQ) — the L-inf and relative differences to
+the order-free exponent-grid sums the device uses.
+
+    python tests/golden/make_longrun.py          (several minutes: the oracle is one core per case)
+"""
+import base64
+import hashlib
+import json
+import os
+import sys
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+LAUNCHES = {"cfg3": 65, "cfg4": 65, "cfg5": 65}
+
+
+def b64(a):
+    return base64.b64encode(np.ascontiguousarray(a).tobytes()).decode()
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def run(name, mode):
+    import oracle_ffi as O
+    from make_fullsize import bench_params
+    cfg = int(name[3:])
+    kw = bench_params(cfg, {})
+    b = O.Batch(O.default_params(**{k: v for k, v in kw.items() if k != "reset_step"}))
+    b.set_reset_step(bool(kw["reset_step"]))
+    if mode != "auto":
+        b.set_q_mode(mode)
+    b.run(LAUNCHES[name])
+    return kw, b
+
+
+def case(name):
+    kw, b = run(name, "auto")
+    q = b.q()
+    fin = np.isfinite(q)
+    out = {"survey_cfg": int(name[3:]), "params": kw, "launches": LAUNCHES[name], "q_repr": b.q_repr(),
+           "q_raw_i64_b64": b64(b.q_raw().astype("<i8")),
+           "n_nan": int(np.isnan(q).sum()), "n_inf": int(np.isinf(q).sum()),
+           "max_abs_finite": float(np.abs(q[fin]).max()) if fin.any() else 0.0,
+           "stats_u64": [int(x) for x in b.stats()[:10]],
+           "eps_sha256": sha(b.lane_eps().astype("<f8"))}
+    if kw.get("selector") == "ucb":
+        n, t = b.ucb()
+        out["ucb_n_u64_b64"] = b64(np.asarray(n, "<u8"))
+        out["ucb_t"] = int(t)
+    # drift measurement: sequential f64 sums (same draws, same mean rule)
+    _, s = run(name, "f64_seq")
+    qs = s.q()
+    both = np.isfinite(q) & np.isfinite(qs)
+    d = np.abs(q[both] - qs[both])
+    out["seq_sum_drift"] = {
+        "nan_masks_equal": bool(np.array_equal(np.isnan(q), np.isnan(qs))),
+        "linf": float(d.max()) if d.size else 0.0,
+        "rel_linf": float((d / np.maximum(np.abs(q[both]), 1.0)).max()) if d.size else 0.0,
+    }
+    return name, out
+
+
+def generate(workers=3):
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        res = dict(ex.map(case, list(LAUNCHES)))
+    return {"source": "tests/golden/make_longrun.py (oracle/rlref.c batched schedule, seed 0x5EED)",
+            **{k: res[k] for k in LAUNCHES}}
+
+
+if __name__ == "__main__":
+    path = os.path.join(HERE, "longrun.json")
+    json.dump(generate(), open(path, "w"), indent=1)
+    print("wrote", path, os.path.getsize(path), "bytes")

@@ -8,8 +8,10 @@ from the reference source, agree bit for bit (VERDICT r01 "next" 9).
   allocations), here on the oracle's RNG stream;
 * tests/golden/faithful_py.py — a plain-Python restatement (cfg 1 sizes).
 
-All run src/agent.rs:66-141 with one_step_agent.rs:48-86 on FrozenLake and
-must end with the same Q bits, rewards and TD errors.
+All run src/agent.rs:66-141 and must end with the same Q bits, rewards and TD
+errors: the C pair on every SURVEY §8(d) configuration family (FrozenLake,
+CliffWalking traces, Taxi UCB + expected SARSA, Blackjack double Q with the
+fxhash observation ids, ...), the Python one on FrozenLake.
 """
 import os
 import subprocess
@@ -28,19 +30,58 @@ CASES = [  # (map8x8, slippery, selector, algo, n_episodes, eval_at)
     (0, 0, "ucb", "qlearning", 300, 30),
     (1, 0, "ucb", "sarsa", 200, 20),
 ]
+ENVS = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}
 SEL = {"eps_greedy": 0, "ucb": 1}
 ALGO = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}
+# the other §8(d) families: (env, agent, policy, selector, algo, n_episodes, eval_at)
+OTHER = [
+    ("cliff_walking", "traces", "tabular", "eps_greedy", "sarsa", 300, 30),          # cfg 4
+    ("taxi", "one_step", "tabular", "ucb", "expected_sarsa", 200, 20),              # cfg 3
+    ("blackjack", "one_step", "double", "eps_greedy", "qlearning", 3000, 300),      # cfg 5
+    ("blackjack", "traces", "double", "ucb", "sarsa", 1000, 100),
+    ("taxi", "traces", "double", "eps_greedy", "expected_sarsa", 150, 15),
+    ("cliff_walking", "one_step", "double", "ucb", "qlearning", 300, 30),
+]
 
 
-def _ref_faithful(m8, slip, sel, algo, n, eval_at):
+def _run_xo(env, m8, slip, agent, policy, sel, algo, n, eval_at):
     if not os.path.exists(XO):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    out = subprocess.run([XO, str(m8), str(slip), str(SEL[sel]), str(ALGO[algo]), str(n), str(eval_at), "1", "1",
-                          "1"], check=True, capture_output=True, text=True).stdout.split("\n")
+    out = subprocess.run([XO, str(ENVS[env]), str(m8), str(slip), str(int(agent == "traces")),
+                          str(int(policy == "double")), str(SEL[sel]), str(ALGO[algo]), str(n), str(eval_at), "1",
+                          "1", "1"], check=True, capture_output=True, text=True).stdout.split("\n")
     q = np.array([int(x, 16) for x in out if len(x) == 16], np.uint64).view(np.float64)
     tail = next(x for x in out if x.startswith("episodes")).split()
     return q, dict(episodes=int(tail[1]), errors=int(tail[3]), reward_sum=float(tail[5]),
                    error_sum=float(tail[7]), eps=float(tail[9]))
+
+
+def _ref_faithful(m8, slip, sel, algo, n, eval_at):
+    return _run_xo("frozen_lake", m8, slip, "one_step", "tabular", sel, algo, n, eval_at)
+
+
+def _same(a, b):
+    a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+    return a.shape == b.shape and bool(((a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))).all())
+
+
+@pytest.mark.parametrize("case", OTHER, ids=lambda c: "-".join(map(str, c)))
+def test_ref_faithful_other_envs_equal_oracle_faithful(oracle, case):
+    """CliffWalking traces (FxHashMap trace swept whole), Taxi, Blackjack with the
+    fxhash observation ids and the double policy's two maps: ref_faithful (the
+    CPU baseline's code, on the oracle's RNG) == rlo_faithful bit for bit."""
+    env, agent, policy, sel, algo, n, eval_at = case
+    q, info = _run_xo(env, 0, 0, agent, policy, sel, algo, n, eval_at)
+    p = oracle.default_params(env=env, agent=agent, policy=policy, selector=sel, algo=algo, n_episodes_for_decay=n)
+    f = oracle.Faithful(p)
+    f.train(n, eval_at)
+    assert _same(q, f.q())
+    rh, el, te = f.histories()
+    assert info["episodes"] == len(el) == n and info["errors"] == len(te)
+    es = 0.0
+    for x in te:
+        es += float(x)
+    assert info["error_sum"] == es or (np.isnan(info["error_sum"]) and np.isnan(es))
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(map(str, c)))
