@@ -439,6 +439,10 @@ struct rl_agent {
     uint64_t launches = 0;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    // train()/evaluate() loop control (k_ctl_word): device {done, lanes, status},
+    // two pinned host slots and their events (read one launch behind)
+    int64_t *ctl_d = nullptr, *ctl_h = nullptr;
+    hipEvent_t ctl_ev[2] = {nullptr, nullptr};
     KParams kp{};
     train_launch_fn fn = nullptr;
     dim3 grid, block;
@@ -811,14 +815,17 @@ int launch_apply_kernel(rl_agent *a) {
 // per-entry grid codes) and the SUM words (grid sums / ΔQ, group counts, ΔN, Δt,
 // NaN / inf counts) over every rank.  Exact int64 arithmetic, so Q is
 // bit-identical for any rank count at a fixed global lane set.
+int comm_live(rl_agent *a);
 int allreduce_max(rl_agent *a) {
     if (!a->comm || a->qrepr != RL_QREPR_F64) return RL_OK;
+    if (int rc = comm_live(a)) return rc;
     NCCLC(ncclAllReduce(a->delta_max, a->delta_max, (size_t)a->P * a->S * a->A, ncclInt64, ncclMax, a->comm->comm,
                         a->stream));
     return RL_OK;
 }
 int allreduce_delta(rl_agent *a) {
     if (!a->comm) return RL_OK;   // no communicator: this process's delta is the total
+    if (int rc = comm_live(a)) return rc;
     NCCLC(ncclAllReduce(a->delta, a->delta, a->delta_words, ncclInt64, ncclSum, a->comm->comm, a->stream));
     return RL_OK;
 }
@@ -837,9 +844,14 @@ int launch_and_merge(rl_agent *a) {
     return merge_after_launch(a);
 }
 // sum of a host value over the ranks (1 rank: itself)
+int comm_live(rl_agent *a) {
+    if (a->comm && !a->comm->comm) return fail(RL_E_STATE, "communicator aborted after a fatal error on this rank");
+    return RL_OK;
+}
 int allreduce_u64(rl_agent *a, uint64_t v, uint64_t *sum) {
     *sum = v;
     if (!a->comm) return RL_OK;
+    if (int rc = comm_live(a)) return rc;
     int64_t x = (int64_t)v;
     HIPC(hipMemcpyAsync(a->comm->word, &x, 8, hipMemcpyHostToDevice, a->stream));
     NCCLC(ncclAllReduce(a->comm->word, a->comm->word, 1, ncclInt64, ncclSum, a->comm->comm, a->stream));
@@ -848,36 +860,73 @@ int allreduce_u64(rl_agent *a, uint64_t v, uint64_t *sum) {
     *sum = (uint64_t)x;
     return RL_OK;
 }
+// A rank that fails inside the loop cannot join the next collective: abort its
+// communicator so the peers' RCCL calls fail instead of waiting on it
+int abort_comm(rl_agent *a, int rc) {
+    if (a->comm && a->comm->comm) {
+        (void)ncclCommAbort(a->comm->comm);
+        a->comm->comm = nullptr;
+    }
+    return rc;
+}
 
+enum { CTL_OK = 0, CTL_LAUNCH_CAP = 1, CTL_RECORD_CAP = 2 };
+
+// train() / evaluate(): launch until every lane of every rank is DONE.
+// After each launch a one-block kernel forms the control word {lanes DONE, lanes,
+// status} (k_ctl_word), one 24-byte all-reduce sums it over the ranks and it is
+// copied to pinned host memory.  The host reads launch k's word only after
+// queueing launch k + 1, so the loop never drains the stream: the GPU runs one
+// launch ahead of the exit test.  That launch is a no-op (DONE lanes draw, update
+// and count nothing; an unchanged merge applies zero) except for the step records,
+// so a recording agent reads each word right away.  Every rank reads the same
+// summed word, so all ranks run the same launches and leave together, also on a
+// per-rank condition (the launch cap, the 4 GiB record cap), which travels in the
+// status word.  A HIP / RCCL error aborts the communicator (abort_comm).
 int run_until_done(rl_agent *a, rl_stats *out) {
-    // stats slot 5 counts lanes that are DONE at the end of a launch.  Guards: a
-    // lane needs at most (max_steps + 1) steps per episode, so a call that has
-    // not finished after this many launches is a bug, not a long run.
+    // a lane needs at most (max_steps + 1) steps per episode, so a call that has
+    // not finished after this many launches is a bug, not a long run
     const uint64_t max_launches = 1ull << 22;
+    const bool dump = getenv("RLAMD_DEBUG_LANES") != nullptr;
+    const uint64_t lag = (a->recording || dump) ? 0 : 1;
+    int rc = comm_live(a);
+    if (rc) return rc;
     for (uint64_t launch = 0;; ++launch) {
-        if (launch >= max_launches) return fail(RL_E_STATE, "train/evaluate did not finish (launch cap)");
-        if (a->rec_h.size() * sizeof(rl_step_record) > (1ull << 32))
-            return fail(RL_E_OOM, "recorded stream exceeds 4 GiB: record fewer steps");
+        int64_t status = CTL_OK;
+        if (launch + 1 >= max_launches) status = CTL_LAUNCH_CAP;
+        if ((a->rec_h.size() + (size_t)a->K * a->L) * sizeof(rl_step_record) > (1ull << 32)) status = CTL_RECORD_CAP;
         // done-lane counter (slot 5 of every stats replica) is per launch
-        HIPC(hipMemset2DAsync(&a->stats_d[5], STATS_W * 8, 0, 8, STATS_REP, a->stream));
-        int rc = launch_and_merge(a);
-        if (rc) return rc;
-        std::vector<unsigned long long> st(STATS_W * STATS_REP);
-        HIPC(hipMemcpyAsync(st.data(), a->stats_d, st.size() * 8, hipMemcpyDeviceToHost, a->stream));
-        HIPC(hipStreamSynchronize(a->stream));
-        unsigned long long done = 0;
-        for (uint32_t r = 0; r < STATS_REP; ++r) done += st[r * STATS_W + 5];
-        if (const char *dump = getenv("RLAMD_DEBUG_LANES")) {   // diagnostics: raw lane records per launch
+        if (hipMemset2DAsync(&a->stats_d[5], STATS_W * 8, 0, 8, STATS_REP, a->stream) != hipSuccess)
+            return abort_comm(a, fail(RL_E_HIP, "stats reset"));
+        if ((rc = launch_and_merge(a))) return abort_comm(a, rc);
+        launch_ctl_word(a->kp, a->ctl_d, a->L, status, a->stream);
+        if (hipGetLastError() != hipSuccess) return abort_comm(a, fail(RL_E_HIP, "control word launch"));
+        if (a->comm) {
+            const ncclResult_t nr = ncclAllReduce(a->ctl_d, a->ctl_d, 3, ncclInt64, ncclSum, a->comm->comm, a->stream);
+            if (nr != ncclSuccess) return abort_comm(a, fail(RL_E_RCCL, std::string("control all-reduce: ") +
+                                                                          ncclGetErrorString(nr)));
+        }
+        const uint32_t slot = (uint32_t)(launch & 1u);
+        if (hipMemcpyAsync(a->ctl_h + 3 * slot, a->ctl_d, 24, hipMemcpyDeviceToHost, a->stream) != hipSuccess ||
+            hipEventRecord(a->ctl_ev[slot], a->stream) != hipSuccess)
+            return abort_comm(a, fail(RL_E_HIP, "control word copy"));
+        if (dump) {   // diagnostics: raw lane records per launch
             std::vector<uint4> c(a->L);
             HIPC(hipMemcpy(c.data(), a->core, a->L * 16, hipMemcpyDeviceToHost));
-            if (FILE *f = fopen(dump, "ab")) { fwrite(c.data(), 16, a->L, f); fclose(f); }
+            if (FILE *f = fopen(getenv("RLAMD_DEBUG_LANES"), "ab")) { fwrite(c.data(), 16, a->L, f); fclose(f); }
         }
-        // every rank runs the same number of launches (each one all-reduces):
-        // stop when the lanes of ALL ranks are done
-        uint64_t done_all = 0, lanes_all = 0;
-        if ((rc = allreduce_u64(a, done, &done_all)) || (rc = allreduce_u64(a, a->L, &lanes_all))) return rc;
-        if (done_all >= lanes_all) break;
+        if (launch < lag) continue;
+        const uint32_t rs = (uint32_t)((launch - lag) & 1u);
+        if (hipEventSynchronize(a->ctl_ev[rs]) != hipSuccess) return abort_comm(a, fail(RL_E_HIP, "control word wait"));
+        const int64_t *w = a->ctl_h + 3 * rs;
+        if (w[2] != CTL_OK) {   // some rank hit a cap: every rank stops here
+            HIPC(hipStreamSynchronize(a->stream));
+            return fail(RL_E_STATE, w[2] % 2 ? "train/evaluate did not finish (launch cap)"
+                                             : "recorded stream exceeds 4 GiB on some rank: record fewer steps");
+        }
+        if (w[0] >= w[1]) break;
     }
+    HIPC(hipStreamSynchronize(a->stream));
     if (out) return rl_agent_stats(a, out);
     return RL_OK;
 }
@@ -1156,6 +1205,11 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
         hipMemcpy(a->cdf, a->eh.cdf.data(), a->eh.cdf.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         return bad(fail(RL_E_HIP, "table upload"));
     if (hipMemset(a->stats_d, 0, STATS_W * 8 * STATS_REP) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
+    if ((rc = dalloc(&a->ctl_d, 3))) return bad(rc);
+    if (hipHostMalloc((void **)&a->ctl_h, 6 * 8, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&a->ctl_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a->ctl_ev[1], hipEventDisableTiming) != hipSuccess)
+        return bad(fail(RL_E_HIP, "loop control buffers"));
 
     KParams &p = a->kp;
     p.L = a->L; p.G = a->G; p.K = a->K; p.S = a->S; p.A = a->A; p.P = a->P;
@@ -1199,7 +1253,10 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
-    dfree(a->net_w); dfree(a->feat);
+    dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d);
+    if (a->ctl_h) (void)hipHostFree(a->ctl_h);
+    for (hipEvent_t e : a->ctl_ev)
+        if (e) (void)hipEventDestroy(e);
     if (a->own_stream) (void)hipStreamDestroy(a->own_stream);
     delete a;
 }

@@ -172,6 +172,7 @@ void launch_fq_merge_b(const KParams &p, hipStream_t s);
 void launch_fq_apply(const KParams &p, hipStream_t s);
 void launch_fold_replicas(const KParams &p, hipStream_t s);
 void launch_fold_apply(const KParams &p, hipStream_t s);
+void launch_ctl_word(const KParams &p, int64_t *ctl, uint64_t lanes, int64_t status, hipStream_t s);
 void launch_kat_log(const double *x, double *out, uint32_t n, hipStream_t s);
 void launch_kat_rng(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out, hipStream_t s);
 void launch_kat_ucb(const double *q, const double *nc, const uint64_t *t, double c, double *out,

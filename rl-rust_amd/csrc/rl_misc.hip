@@ -89,6 +89,26 @@ void launch_fill_f64(double *ptr, uint64_t n, double v, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ptr, n, v);
 }
 
+// ---------------------------------------------------------------- loop control word
+// train()/evaluate()'s exit agreement, formed on the device after each launch:
+// ctl = {lanes DONE (stats slot 5 over the replicas), lanes, status}; the caller
+// sums it over the ranks (one 24-byte all-reduce) and reads it one launch later.
+__global__ void __launch_bounds__(64) k_ctl_word(const unsigned long long *stats, int64_t *ctl, uint64_t lanes,
+                                                 int64_t status) {
+    const uint32_t t = threadIdx.x;
+    uint64_t v = 0;
+    for (uint32_t r = t; r < STATS_REP; r += 64u) v += stats[(uint64_t)r * STATS_W + 5u];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (t == 0) {
+        ctl[0] = (int64_t)v;
+        ctl[1] = (int64_t)lanes;
+        ctl[2] = status;
+    }
+}
+void launch_ctl_word(const KParams &p, int64_t *ctl, uint64_t lanes, int64_t status, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctl_word, dim3(1), dim3(64), 0, s, p.stats, ctl, lanes, status);
+}
+
 // ---------------------------------------------------------------- replica fold
 // delta += sum over replicas (exact int64), replicas zeroed for the next launch.
 // Block = 64 words x 4 replica slices; each thread's replica loads are
