@@ -46,6 +46,11 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
     const uint32_t pd = row >> 1, p = pd / 11u, d = pd - p * 11u;
     return ((p << 5) + d) * 2u + (row & 1u);
 }
+// Pair traces on small tables (FrozenLake, CliffWalking: S*A <= 256, so a pair id
+// is 8 bits) keep every wave's visited pairs in one pool (pair_pool below)
+__host__ __device__ constexpr bool pair_pool_env(int env) {
+    return env == RL_ENV_CLIFF_WALKING || env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED;
+}
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   misc u32[4]            f64 traces: the group step's max td code
 //   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40, or f64 bits)
@@ -62,7 +67,8 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 //   tr   env transition table (FrozenLake / CliffWalking; Taxi computes its
 //        transitions and reads its start cdf from HBM, Blackjack has none)
 //   trc  pair traces (traces == 2): the first trc_cap slots of every lane's pair
-//        list, ids u16 [cap][nthr] then E f64 [cap][nthr] (column = thread)
+//        list, ids u16 [cap][nthr] then E f64 [cap][nthr] (column = thread);
+//        small tables: the first trc_cap items of every wave's pair pool
 // nthr = the shared kernel's block size; 0 for the private kernel (tables only).
 // traces: 0 none, 1 whole-row visited-state sets, 2 visited-pair sets
 // ucb: 0 none, 1 UCB, 2 UCB + expected SARSA (launch counts u32 [S][A] + step
@@ -102,13 +108,21 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     // trc_kb KiB per group (KParams::trc_kb), at most S*A slots per lane
     // row strides padded by 2 / 1 entries (PairCache): one lane's consecutive
     // slots then sit in different LDS banks
-    if (shared_q && traces == 2) {
+    // pool form (small tables, pair_pool): trc_cap = items per wave, tags u16
+    // [waves][cap] then E f64 [waves][cap]
+    const bool pool = shared_q && traces == 2 && pair_pool_env(env);
+    if (pool) {
+        const uint32_t nw = nthr >> 6, c = trc_kb * 1024u / (nw * 10u);
+        l.trc_cap = c < 64u * S * A ? c : 64u * S * A;
+    } else if (shared_q && traces == 2) {
         const uint32_t c = trc_kb * 1024u / ((nthr + 2u) * 2u + (nthr + 1u) * 8u);
         l.trc_cap = c < S * A ? c : S * A;
     } else {
         l.trc_cap = 0u;
     }
-    l.trc = off; off += l.trc_cap ? align16(l.trc_cap * (nthr + 2u) * 2u) + l.trc_cap * (nthr + 1u) * 8u : 0u;
+    l.trc = off;
+    if (pool) off += l.trc_cap ? align16(l.trc_cap * (nthr >> 6) * 2u) + l.trc_cap * (nthr >> 6) * 8u : 0u;
+    else off += l.trc_cap ? align16(l.trc_cap * (nthr + 2u) * 2u) + l.trc_cap * (nthr + 1u) * 8u : 0u;
     l.total = off;
     return l;
 }
@@ -663,7 +677,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if constexpr (TRACES) tcnt = active ? p.tcnt[lane] : 0u;
     const PairCache pc{(uint16_t *)(smem + lay.trc), (double *)(smem + lay.trc + align16(lay.trc_cap * (nthr + 2u) * 2u)),
                        lay.trc_cap, nthr, tid};
-    if constexpr (PAIRS) { if (active) pair_cache_load(p, pc, lane, tcnt); }
     // small tables (S*A <= 256: FrozenLake, CliffWalking): the lane's visited-pair set
     // as a bitmap in registers, rebuilt from the list at launch start.  A visit then
     // needs no scan: a new pair is appended, a visited one gets its E += 1 inside the
@@ -673,6 +686,24 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                            (ENV == RL_ENV_CLIFF_WALKING || ENV == RL_ENV_FROZEN_LAKE ||
                             ENV == RL_ENV_FROZEN_LAKE_EDITED);
     constexpr int PBW = ENV == RL_ENV_CLIFF_WALKING ? 6 : 8;   // 48*4 / 64*4 pair ids
+    // pair pool (small tables): the visited pairs of a wave's 64 lanes as ONE list of
+    // items, tag = pair id (8 bits) | lane in wave << 8 | first-of-state << 15, and
+    // its E.  A step sweeps the pool 64 items per round, every thread one item (no
+    // per-lane list walk, no owner search), and compacts it in place (the items of
+    // lanes whose episode ended leave); a new pair contributes from its own lane and
+    // joins at the end.  Items [0, trc_cap) in LDS, the rest in HBM at the same index
+    // of the wave's lanes' pair rows (p.tlist / p.trace, lane-major, so the wave's
+    // rows are one region of 64*S*A >= any pool); the count in p.tcnt[first lane].
+    constexpr bool POOL = PAIRS && pair_pool_env(ENV);
+    static_assert(!POOL || (PBITS && A == 4), "pair pool: small-table pair bits");
+    const uint32_t pw = tid >> 6, plid = tid & 63u;
+    const uint64_t plane0 = (uint64_t)blockIdx.x * p.G + (uint64_t)pw * p.lpw;
+    const bool pwave = (uint64_t)pw * p.lpw < p.G && plane0 < p.L;   // the wave holds lanes
+    uint16_t *const PT = (uint16_t *)(smem + lay.trc) + pw * lay.trc_cap;
+    double *const PE = (double *)(smem + lay.trc + align16(lay.trc_cap * (nthr >> 6) * 2u)) + pw * lay.trc_cap;
+    uint16_t *const HT = p.tlist + plane0 * SA;
+    double *const HE = p.trace + plane0 * SA;
+    uint32_t npool = 0;
     uint32_t pbits[PBW];
 #pragma unroll
     for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
@@ -686,7 +717,29 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
         for (int i = 0; i < PBW; ++i) pbits[i] |= (id >> 5) == (uint32_t)i ? (1u << (id & 31u)) : 0u;
     };
-    if constexpr (PBITS) {
+    if constexpr (PAIRS && !POOL) { if (active) pair_cache_load(p, pc, lane, tcnt); }
+    if constexpr (POOL) {
+        npool = pwave ? p.tcnt[plane0] : 0u;
+        const uint32_t nl = npool < lay.trc_cap ? npool : lay.trc_cap;
+        for (uint32_t q = plid; q < nl; q += 64u) {
+            PT[q] = HT[q];
+            PE[q] = HE[q];
+        }
+        __syncthreads();
+        // every lane's pair bits from the pool (each lane reads every tag: broadcast)
+        constexpr uint32_t TB = 8;
+        for (uint32_t q0 = 0; q0 < npool; q0 += TB) {
+            uint32_t t[TB];
+#pragma unroll
+            for (uint32_t k = 0; k < TB; ++k) {
+                const uint32_t q = q0 + k < npool ? q0 + k : q0;
+                t[k] = q < lay.trc_cap ? (uint32_t)PT[q] : (uint32_t)HT[q];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < TB; ++k)
+                if (q0 + k < npool && ((t[k] >> 8) & 63u) == plid) pbits_set(t[k] & 0xffu);
+        }
+    } else if constexpr (PBITS) {
         static_assert(A == 4, "a state's pair bits sit in one bitmap word");
         if (active)
             for (uint32_t j = 0; j < tcnt; ++j)
@@ -1127,7 +1180,99 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 __syncthreads();
                 e_tr = fq_grid(GCODE[0]) + p.trace_k;
             }
-            if constexpr (PAIRS && RLAMD_COOP_SWEEP) {
+            // a visited state's row count n += 1 (settle_row's mean)
+            auto row_hit = [&](uint32_t rid) {
+                if (rsweep) atomicAdd(&CNTR[rid], 1u);
+                else if (atomicAdd(&CNTR[rid], 1u) == 0u) LIST[atomicAdd(&LISTN[0], 1u)] = (uint16_t)rid;
+            };
+            if constexpr (POOL) {
+                // this lane's visit: a visited pair gets its E += 1 inside the sweep (hid);
+                // a new pair contributes below with E = 1 and then joins the pool
+                uint32_t hid = 0x1ffu, nid = 0u;
+                bool newp = false, first_new = false;
+                if (train) {
+                    const uint32_t id = L.s * (uint32_t)A + L.a;
+                    const uint32_t w = pbits_word(id >> 5);
+                    if ((w >> (id & 31u)) & 1u) {
+                        hid = id;
+                    } else {
+                        newp = true;
+                        nid = id;
+                        first_new = ((w >> ((L.s * (uint32_t)A) & 31u)) & 0xfu) == 0u;
+                        pbits_set(id);
+                    }
+                }
+                const uint64_t trM = __ballot(train), tmM = __ballot(train && term);
+                const uint32_t pk = hid | (ut << 16);
+                const uint32_t C = lay.trc_cap;
+                const uint64_t below = (1ull << plid) - 1ull;
+                uint32_t wpos = 0;                             // items kept so far (uniform)
+                constexpr uint32_t U = RLAMD_SWEEP_U;
+                for (uint32_t q0 = 0; q0 < npool; q0 += 64u * U) {
+                    uint32_t tg[U], pkv[U];
+                    double ev[U], tdv[U];
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t q = q0 + 64u * u + plid;
+                        tg[u] = 0u;
+                        ev[u] = 0.0;
+                        if (q < npool) {
+                            const bool in = q < C;
+                            tg[u] = in ? (uint32_t)PT[q] : (uint32_t)HT[q];
+                            ev[u] = in ? PE[q] : HE[q];
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const int il = (int)((tg[u] >> 8) & 63u);
+                        tdv[u] = __shfl(td, il, 64);
+                        pkv[u] = (uint32_t)__shfl((int)pk, il, 64);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) {
+                        const uint32_t q = q0 + 64u * u + plid, il = (tg[u] >> 8) & 63u;
+                        const bool valid = q < npool;
+                        const bool istr = valid && ((trM >> il) & 1ull);
+                        const bool keep = valid && !((tmM >> il) & 1ull);
+                        double en = ev[u];
+                        if (istr) {
+                            const uint32_t id = tg[u] & 0xffu, uto = pkv[u] >> 16;
+                            const double e1 = id == (pkv[u] & 0x1ffu) ? ev[u] + 1.0 : ev[u];
+                            const uint32_t o = id >> 2, b = id & 3u;   // A == 4
+                            if (tg[u] & 0x8000u) {
+                                ++trace_states;
+                                row_hit(uto * SL + lrow(o));
+                            }
+                            contrib_tr(qi(uto, o, b), p.lr * (tdv[u] * e1), e_tr);
+                            en = e1 * p.gl;
+                        }
+                        const uint64_t m = __ballot(keep);
+                        const uint32_t pos = wpos + (uint32_t)__popcll(m & below);
+                        if (keep) {
+                            if (pos < C) { PT[pos] = (uint16_t)tg[u]; PE[pos] = en; }
+                            else { HT[pos] = (uint16_t)tg[u]; HE[pos] = en; }
+                        }
+                        wpos += (uint32_t)__popcll(m);
+                    }
+                }
+                if (newp) {
+                    if (first_new) {
+                        ++trace_states;
+                        row_hit(ut * SL + lrow(L.s));
+                    }
+                    contrib_tr(qi(ut, L.s, L.a), p.lr * (td * 1.0), e_tr);
+                }
+                const bool keepn = newp && !term;
+                const uint64_t m = __ballot(keepn);
+                if (keepn) {
+                    const uint32_t pos = wpos + (uint32_t)__popcll(m & below);
+                    const uint16_t tag = (uint16_t)(nid | (plid << 8) | (first_new ? 0x8000u : 0u));
+                    const double en = 1.0 * p.gl;
+                    if (pos < C) { PT[pos] = tag; PE[pos] = en; }
+                    else { HT[pos] = tag; HE[pos] = en; }
+                }
+                npool = wpos + (uint32_t)__popcll(m);
+            } else if constexpr (PAIRS && RLAMD_COOP_SWEEP) {
                 uint32_t hid = 0xffffu;      // PBITS: the visited pair whose E += 1 the sweep applies
                 if constexpr (PBITS) {
                     if (train) {
@@ -1282,7 +1427,21 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 // a non-finite td also moves the never-taken actions of every visited
                 // state, whose E is 0: lr * (td * 0) is NaN (elegibility_traces_agent.rs:
                 // 86-96 sweeps whole rows); the pair lists hold only taken actions
-                if (train && !__builtin_isfinite(td)) {
+                if (POOL && train && !__builtin_isfinite(td)) {
+                    // the lane's visited states are its pair bits: A == 4 bits per state
+                    const double dn = p.lr * (td * 0.0);
+#pragma unroll
+                    for (int wi = 0; wi < PBW; ++wi) {
+                        const uint32_t w = opq(pbits[wi]);
+                        for (uint32_t k = 0; k < 8u; ++k) {
+                            const uint32_t bits = (w >> (4u * k)) & 0xfu;
+                            if (!bits) continue;
+                            const uint32_t o = (uint32_t)wi * 8u + k;
+                            for (uint32_t b = 0; b < 4u; ++b)
+                                if (!((bits >> b) & 1u)) contrib_tr(qi(ut, o, b), dn, e_tr);
+                        }
+                    }
+                } else if (train && !__builtin_isfinite(td)) {
                     const double dn = p.lr * (td * 0.0);
                     auto id_at = [&](uint32_t j) -> uint32_t {
                         return j < pc.cap ? (uint32_t)pc.TRI[pc.ixi(j)] : (uint32_t)p.tlist[pslot(p, j, lane)];
@@ -1305,7 +1464,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     }
                 }
                 if (train && term) {
-                    pair_clear(p, pc, lane, tcnt);
+                    if constexpr (!POOL) pair_clear(p, pc, lane, tcnt);
                     if constexpr (PBITS) {
 #pragma unroll
                         for (int i = 0; i < PBW; ++i) pbits[i] = 0u;
@@ -1372,8 +1531,17 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
 
     if (active) lane_store(p, lane, L);
-    if constexpr (TRACES) { if (active) p.tcnt[lane] = tcnt; }
-    if constexpr (PAIRS) { if (active) pair_cache_store(p, pc, lane, tcnt); }
+    if constexpr (POOL) {
+        const uint32_t nl = npool < lay.trc_cap ? npool : lay.trc_cap;
+        for (uint32_t q = plid; q < nl; q += 64u) {
+            HT[q] = PT[q];
+            HE[q] = PE[q];
+        }
+        if (plid == 0 && pwave) p.tcnt[plane0] = npool;
+    } else {
+        if constexpr (TRACES) { if (active) p.tcnt[lane] = tcnt; }
+        if constexpr (PAIRS) { if (active) pair_cache_store(p, pc, lane, tcnt); }
+    }
     {
         const uint32_t c_done = (uint32_t)__popcll(__ballot(active && L.mode == RL_MODE_DONE));
         if ((tid & 63u) == 0) {
