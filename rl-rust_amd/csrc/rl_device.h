@@ -22,23 +22,31 @@ constexpr double MIN_POSITIVE = 2.2250738585072014e-308;  // f64::MIN_POSITIVE
 // Replaces rand::thread_rng() (entropy-seeded ChaCha12) at the reference's draw
 // sites with one xoshiro128+ stream per lane, keyed (seed, global lane id).  Every
 // draw site uses the words' high bits; '+' costs one VALU op of output mixing.
+// three-input XOR in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96
+// (the compiler does not form it from a ^ b ^ c)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 struct Rng {
     uint32_t s0, s1, s2, s3;
+    // xoshiro128 state transition written on the old words (s2 ^= s0; s3 ^= s1;
+    // s1 ^= s2; s0 ^= s3; s2 ^= s1 << 9; s3 = rotl(s3, 11)): three xor3 + one xor
+    // + the shift and the rotate
+    __device__ __forceinline__ void advance() {
+        const uint32_t t = s1 << 9;
+        const uint32_t n1 = xor3(s1, s2, s0), n2 = xor3(s2, s0, t), n0 = xor3(s0, s3, s1), n3 = s3 ^ s1;
+        s0 = n0; s1 = n1; s2 = n2;
+        s3 = __builtin_rotateleft32(n3, 11);
+    }
     __device__ __forceinline__ uint32_t next_u32() {
         const uint32_t r = s0 + s3;
-        const uint32_t t = s1 << 9;
-        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3;
-        s2 ^= t;
-        s3 = __builtin_rotateleft32(s3, 11);
+        advance();
         return r;
     }
     // advance as next_u32 does, without the output scrambler (a draw whose value is unused)
-    __device__ __forceinline__ void skip_u32() {
-        const uint32_t t = s1 << 9;
-        s2 ^= s0; s3 ^= s1; s1 ^= s2; s0 ^= s3;
-        s2 ^= t;
-        s3 = __builtin_rotateleft32(s3, 11);
-    }
+    __device__ __forceinline__ void skip_u32() { advance(); }
     // RngCore::next_u64 of a 32-bit block generator: low word first
     __device__ __forceinline__ uint64_t next_u64() {
         const uint64_t lo = next_u32();
