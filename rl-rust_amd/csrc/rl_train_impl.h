@@ -728,13 +728,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         __syncthreads();
         // every lane's pair bits from the pool (each lane reads every tag: broadcast)
         constexpr uint32_t TB = 8;
-        for (uint32_t q0 = 0; q0 < npool; q0 += TB) {
+        for (uint32_t q0 = 0; q0 < nl; q0 += TB) {
             uint32_t t[TB];
 #pragma unroll
-            for (uint32_t k = 0; k < TB; ++k) {
-                const uint32_t q = q0 + k < npool ? q0 + k : q0;
-                t[k] = q < lay.trc_cap ? (uint32_t)PT[q] : (uint32_t)HT[q];
-            }
+            for (uint32_t k = 0; k < TB; ++k) t[k] = PT[q0 + k < nl ? q0 + k : q0];
+#pragma unroll
+            for (uint32_t k = 0; k < TB; ++k)
+                if (q0 + k < nl && ((t[k] >> 8) & 63u) == plid) pbits_set(t[k] & 0xffu);
+        }
+        for (uint32_t q0 = nl; q0 < npool; q0 += TB) {
+            uint32_t t[TB];
+#pragma unroll
+            for (uint32_t k = 0; k < TB; ++k) t[k] = HT[q0 + k < npool ? q0 + k : q0];
 #pragma unroll
             for (uint32_t k = 0; k < TB; ++k)
                 if (q0 + k < npool && ((t[k] >> 8) & 63u) == plid) pbits_set(t[k] & 0xffu);
@@ -1211,15 +1216,26 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 for (uint32_t q0 = 0; q0 < npool; q0 += 64u * U) {
                     uint32_t tg[U], pkv[U];
                     double ev[U], tdv[U];
+                    // items past the LDS part only in a wave-uniform slow path (a per-item
+                    // select let the compiler load both copies of every item)
+                    if (q0 + 64u * U <= C) {
 #pragma unroll
-                    for (uint32_t u = 0; u < U; ++u) {
-                        const uint32_t q = q0 + 64u * u + plid;
-                        tg[u] = 0u;
-                        ev[u] = 0.0;
-                        if (q < npool) {
-                            const bool in = q < C;
-                            tg[u] = in ? (uint32_t)PT[q] : (uint32_t)HT[q];
-                            ev[u] = in ? PE[q] : HE[q];
+                        for (uint32_t u = 0; u < U; ++u) {
+                            const uint32_t q = q0 + 64u * u + plid;
+                            const uint32_t qc = q < npool ? q : 0u;
+                            tg[u] = PT[qc];
+                            ev[u] = PE[qc];
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t u = 0; u < U; ++u) {
+                            const uint32_t q = q0 + 64u * u + plid;
+                            tg[u] = 0u;
+                            ev[u] = 0.0;
+                            if (q < npool) {
+                                if (q < C) { tg[u] = PT[q]; ev[u] = PE[q]; }
+                                else { tg[u] = HT[q]; ev[u] = HE[q]; }
+                            }
                         }
                     }
 #pragma unroll
@@ -1249,7 +1265,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         const uint64_t m = __ballot(keep);
                         const uint32_t pos = wpos + (uint32_t)__popcll(m & below);
                         if (keep) {
-                            if (pos < C) { PT[pos] = (uint16_t)tg[u]; PE[pos] = en; }
+                            if (wpos + 64u <= C || pos < C) { PT[pos] = (uint16_t)tg[u]; PE[pos] = en; }
                             else { HT[pos] = (uint16_t)tg[u]; HE[pos] = en; }
                         }
                         wpos += (uint32_t)__popcll(m);
