@@ -49,7 +49,9 @@ def one(cfg):
     a.set_stream(s.cuda_stream)
     a.run(2)
     out = {"cfg": cfg, "q_repr": a.q_repr(), "lanes": kw["n_lanes"],
-           "merge_bytes": 8 * (a.delta_words() + (a.delta_max_words() if a.q_repr() == "f64" else 0))}
+           # bytes all-reduced per merge: MAX words (f64 only) and SUM words
+           "max_bytes": 8 * a.delta_max_words() if a.q_repr() == "f64" else 0,
+           "sum_bytes": 8 * (a.delta_words() - a.delta_max_words())}
     out["train_launch_ms"], _ = timed(s, a.launch_train, 32)
     a.sync()
     out["merge_local_ms"], out["merge_local_host_ms"] = timed(s, a.sync)
