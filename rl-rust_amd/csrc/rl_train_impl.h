@@ -1445,14 +1445,19 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 // 86-96 sweeps whole rows); the pair lists hold only taken actions
                 if (POOL && train && !__builtin_isfinite(td)) {
                     // the lane's visited states are its pair bits: A == 4 bits per state
+                    // (rare: kept rolled — unrolled it was 2.4k instructions inside the step loop)
                     const double dn = p.lr * (td * 0.0);
-#pragma unroll
-                    for (int wi = 0; wi < PBW; ++wi) {
-                        const uint32_t w = opq(pbits[wi]);
-                        for (uint32_t k = 0; k < 8u; ++k) {
+#pragma unroll 1
+                    for (uint32_t wi = 0; wi < (uint32_t)PBW; ++wi) {
+                        const uint32_t w = pbits_word(wi);
+                        uint32_t m = w;
+#pragma unroll 1
+                        while (m) {
+                            const uint32_t k = (uint32_t)__builtin_ctz(m) >> 2;
                             const uint32_t bits = (w >> (4u * k)) & 0xfu;
-                            if (!bits) continue;
-                            const uint32_t o = (uint32_t)wi * 8u + k;
+                            m &= ~(0xfu << (4u * k));
+                            const uint32_t o = wi * 8u + k;
+#pragma unroll 1
                             for (uint32_t b = 0; b < 4u; ++b)
                                 if (!((bits >> b) & 1u)) contrib_tr(qi(ut, o, b), dn, e_tr);
                         }
