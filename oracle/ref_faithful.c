@@ -36,7 +36,10 @@
  * Not modelled: kdam's progress bar (one counter update per episode).
  *
  * Build with -DRF_XOSHIRO (linked with rlref.c) to replace ChaCha12 by the
- * oracle's per-lane xoshiro128+ stream and libm's ln by the
+ * oracle's per-lane xoshiro128+ stream (which also skips the
+ * draws whose values the reference never looks at: FrozenLake's reset and
+ * deterministic-map step draws, and the low word of a power-of-two action
+ * draw) and libm's ln by the
  * oracle's fdlibm one (a last-ulp difference at some t reaches UCB + expected
  * SARSA's probabilities): the run is then bit-identical to
  * oracle/rlref.c's rlo_faithful loop, which tests/test_oracle_cross.py checks —
@@ -127,6 +130,11 @@ static inline double unif01(rng_t *r) {
     return b.d - 1.0;
 }
 static inline uint32_t unif_action(rng_t *r, uint32_t n) {
+#ifdef RF_XOSHIRO
+    /* the oracle's stream: a power-of-two range takes one u32's top bits (the
+     * u64's low word is never looked at; rlref.c uniform_action) */
+    if (n >= 2 && (n & (n - 1)) == 0) return rng_u32(r) >> (32 - __builtin_ctz(n));
+#endif
     const uint64_t range = n, zone = UINT64_MAX - (UINT64_MAX - range + 1) % range;
     for (;;) {
         unsigned __int128 m = (unsigned __int128)rng_u64(r) * range;
@@ -235,6 +243,7 @@ typedef struct {
     uint8_t player[16], dealer[16];   /* Blackjack */
     size_t pi, di;
     int pace, dace;
+    int slippery;                  /* FrozenLake is_slippery */
 } env_t;
 static const char *MAP4[] = {"SFFF", "FHFH", "FFFH", "HFFG"};                              /* frozen_lake.rs:23 */
 static const char *MAP8[] = {"SFFFFFFF", "FFFFFFFF", "FFFHFFFF", "FFFFFHFF", "FFFHFFFF", "FHHFFFHF",
@@ -274,6 +283,7 @@ static void env_new(env_t *e, int kind, int map8, int slippery, uint64_t max_ste
     memset(e, 0, sizeof *e);
     e->kind = kind;
     e->max_steps = max_steps;
+    e->slippery = slippery;
     if (kind == ENV_FL) {                                                                     /* frozen_lake.rs:48-102 */
         const char **map = map8 ? MAP8 : MAP4;
         const int n = map8 ? 8 : 4;
@@ -375,7 +385,11 @@ static uint64_t env_reset(env_t *e, rng_t *g) {
     e->ready = 1;
     e->curr_step = 0;
     if (e->kind == ENV_FL) {                                                                  /* frozen_lake.rs:106-113 */
+#ifdef RF_XOSHIRO
+        const double u = 0.0;   /* the oracle's stream: the one-'S' maps' draw is never looked at */
+#else
         const double u = unif01(g);
+#endif
         double *v = (double *)malloc(e->ns * sizeof(double));   /* initial_state_distrib.to_vec() */
         memcpy(v, e->start, e->ns * sizeof(double));
         e->pos = categorical_sample(v, e->ns, u);
@@ -429,7 +443,11 @@ static int env_step(env_t *e, uint32_t a, rng_t *g, uint64_t *s2, double *r, int
         transition tr[3];
         memcpy(tr, e->probs[e->pos][a], sizeof tr);
         const double tp[3] = {tr[0].p, tr[1].p, tr[2].p};
-        const double u = unif01(g);
+#ifdef RF_XOSHIRO
+        const double u = e->slippery ? unif01(g) : 0.0;   /* the oracle's stream: no unused draw */
+#else
+        const double u = unif01(g);                        /* drawn even when not slippery */
+#endif
         const uint64_t i = categorical_sample(tp, 3, u);
         e->pos = tr[i].s;
         if (tr[i].t) e->ready = 0;

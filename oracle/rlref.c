@@ -316,7 +316,12 @@ uint32_t rlo_uniform_int_u64(uint64_t v, uint64_t range, int *reject) {
     *reject = !(lo <= zone);
     return (uint32_t)hi;
 }
+/* A a power of two: the zone rejects nothing and the value is the top log2(A)
+ * bits of next_u64's HIGH word — the low word is never looked at — so the
+ * stream draws one u32 and takes its top bits: the same uniform over 0..A
+ * (DESIGN.md §2 "draws"; device: rl_device.h uniform_action). */
 static uint32_t uniform_action(rlo_rng *r, uint32_t A) {
+    if (A >= 2 && (A & (A - 1)) == 0) return next_u32(r) >> (32 - __builtin_ctz(A));
     for (;;) {
         int rej;
         uint32_t a = rlo_uniform_int_u64(next_u64(r), A, &rej);
@@ -443,6 +448,8 @@ typedef struct {
     int trunc_stay;      /* truncation observes the current position (FrozenLakeEdited) instead of 0 */
     uint32_t nrow, ncol; /* grid envs */
     const char **map;    /* FrozenLake maps */
+    int slippery;        /* FrozenLake family: is_slippery (the step's draw is used) */
+    int32_t fixed_start; /* >= 0: the start distribution is one state (no reset draw) */
 } envdef;
 
 typedef struct {
@@ -624,10 +631,7 @@ static void build_taxi(envdef *E) {
     E->trunc_reward = 0.0; /* taxi.rs:146-149 */
 }
 
-static int build_env(envdef *E, const rlo_config *c) {
-    memset(E, 0, sizeof(*E));
-    E->kind = c->env;
-    E->max_steps = c->max_steps;
+static int build_env_tables(envdef *E, const rlo_config *c) {
     switch (c->env) {
     case RLO_ENV_FROZEN_LAKE: build_frozen_lake(E, c->map8x8, c->slippery); return 0;
     case RLO_ENV_FROZEN_LAKE_EDITED: build_frozen_lake_edited(E, c->map8x8, c->slippery); return 0;
@@ -636,6 +640,19 @@ static int build_env(envdef *E, const rlo_config *c) {
     case RLO_ENV_BLACKJACK: E->S = 32 * 32 * 2; E->A = 2; return 0;
     }
     return -1;
+}
+static int build_env(envdef *E, const rlo_config *c) {
+    memset(E, 0, sizeof(*E));
+    E->kind = c->env;
+    E->max_steps = c->max_steps;
+    if (build_env_tables(E, c)) return -1;
+    E->slippery = c->slippery != 0;
+    /* one state of probability 1: categorical_sample (utils.rs:33-43) returns it for every u */
+    uint32_t nz = 0, at = 0;
+    for (uint32_t i = 0; i < E->n_start; ++i)
+        if (E->start[i] != 0.0) { nz++; at = i; }
+    E->fixed_start = (nz == 1 && E->start[at] == 1.0) ? (int32_t)at : -1;
+    return 0;
 }
 
 int rlo_env_dims(const rlo_config *c, uint32_t *S, uint32_t *A) {
@@ -681,6 +698,10 @@ static uint32_t env_reset(const envdef *E, envstate *st, rlo_rng *r) {
     }
     if (E->kind == RLO_ENV_CLIFF_WALKING) {
         st->pos = 36;
+    } else if (E->fixed_start >= 0) {
+        /* one start state (FrozenLake's maps): categorical_sample returns it for
+         * every u, so the reference's draw (frozen_lake.rs:107-108) is not made */
+        st->pos = (uint32_t)E->fixed_start;
     } else {
         double u = uniform01(r);
         st->pos = categorical_sample(E->start, E->n_start, u);
@@ -730,8 +751,10 @@ static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint3
     st->curr_step += 1;
     size_t k = ((size_t)st->pos * E->A + a) * 3;
     uint32_t i = 0;
-    if (E->kind == RLO_ENV_FROZEN_LAKE || E->kind == RLO_ENV_FROZEN_LAKE_EDITED) {
-        double u = uniform01(r);                       /* one draw even when not slippery */
+    if ((E->kind == RLO_ENV_FROZEN_LAKE || E->kind == RLO_ENV_FROZEN_LAKE_EDITED) && E->slippery) {
+        /* the reference draws here on deterministic maps too (frozen_lake.rs:126),
+         * a value categorical_sample([1, 0, 0]) ignores: not made there */
+        double u = uniform01(r);
         i = categorical_sample(&E->prob[k], 3, u);
     }
     st->pos = E->next[k + i];

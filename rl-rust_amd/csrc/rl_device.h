@@ -76,8 +76,13 @@ __device__ __forceinline__ double uniform01(Rng &r) {
 }
 // rand 0.8.5 UniformInt<usize>::sample for Uniform::from(0..A)
 // (uniform_epsilon_greed.rs:34,62): widening multiply, reject lo > zone.
+// A power of two (FrozenLake / CliffWalking 4, Blackjack 2): the zone rejects
+// nothing and the result is the top log2(A) bits of next_u64's high word, whose
+// low word is never looked at — so the stream draws ONE u32 and takes its top
+// bits (the same uniform distribution over 0..A; DESIGN §2 "draws").
 template <uint32_t A>
 __device__ __forceinline__ uint32_t uniform_action(Rng &r) {
+    if constexpr (A >= 2u && (A & (A - 1u)) == 0u) return r.next_u32() >> (32 - __builtin_ctz(A));
     constexpr uint64_t reject = (0ull - (uint64_t)A) % (uint64_t)A;  // (MAX - A + 1) % A
     constexpr uint64_t zone = ~0ull - reject;
     for (;;) {
@@ -544,8 +549,8 @@ template <bool AM, int A>
 __device__ __forceinline__ uint32_t tidx(const EnvTables &t, uint32_t s, uint32_t a) {
     return AM ? a * t.S + s : s * (uint32_t)A + a;
 }
-// Env::reset's categorical draw (frozen_lake.rs:107-108, taxi.rs:136-137): the
-// uniform is always consumed; the search is skipped when the answer is fixed.
+// Env::reset's categorical draw (taxi.rs:136-137): the search is skipped when
+// the answer is fixed.
 __device__ __forceinline__ uint32_t start_state(const EnvTables &t, double u) {
     return t.fixed_start >= 0 ? (uint32_t)t.fixed_start : cdf_search(t.cdf, t.n_start, u);
 }
@@ -555,11 +560,13 @@ template <int ENV> struct EnvDev;
 // FrozenLakeEnv (src/env/frozen_lake.rs).  trans[s*4+a]: 3 outcome bytes
 // (bits 0-5 next, bit 6 reward==1.0, bit 7 terminated) + bit 24 "slippery row".
 // One synchronous step of a FrozenLake-family lane that either RESETs (doR) or
-// STEPs (doS), without branching on which: both consume exactly one uniform
-// (reset :107-108 / :222-223, step :126 / :235) unless the step truncates, so
-// the draw is one masked block for the wave, and the table word is read by
-// every lane (pos and a are always valid indices).  Truncation: (0, 0.0, true)
-// for FrozenLake (:119-122), (pos, -1.0, true) for FrozenLakeEdited (:227-231).
+// STEPs (doS), without branching on which.  Only a step on a slippery map
+// draws (:126 / :235): the reference also draws at reset (:107-108 / :222-223,
+// the one-'S' maps' categorical always returns 0) and on deterministic maps,
+// values it never looks at, which the stream skips (DESIGN §2 "draws").  The
+// table word is read by every lane (pos and a are always valid indices).
+// Truncation: (0, 0.0, true) for FrozenLake (:119-122), (pos, -1.0, true) for
+// FrozenLakeEdited (:227-231).
 // The outcome byte's reward bit means 1.0 (FrozenLake) or 10.0 (edited; else -1.0).
 template <bool EDITED, int SLIP, bool AM>
 __device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
@@ -568,13 +575,10 @@ __device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, ui
     const bool st = doS && !trunc;
     const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
     uint32_t i = 0;
-    if (doR || st) {
-        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {
+    if (SLIP == 1 || (SLIP < 0 && t.slippery)) {      // the only draw whose value is used
+        if (st) {
             const double u = uniform01(r);
-            if (st && (w & (1u << 24))) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
-        } else {
-            r.skip_u32();
-            r.skip_u32();
+            if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
         }
     }
     const uint32_t o = (w >> (8 * i)) & 0xffu;
@@ -588,15 +592,13 @@ __device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, ui
 
 // Both built-in maps (MAP_4X4 / MAP_8X8) have one 'S', at position 0, so
 // Env::reset's categorical draw always returns 0 (the host asserts this): the
-// draw is consumed without computing its value.  SLIP: the map's slippery
+// draw is not made (its value is never used).  SLIP: the map's slippery
 // flag as a compile-time constant (0 / 1), or -1 to read it at run time.
 template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
     static constexpr int A = 4;
-    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &) {
-        r.skip_u32();                                  // frozen_lake.rs:107-108: one uniform,
-        r.skip_u32();                                  // categorical_sample -> 0
-        z = 0;
-        return 0u;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &, const EnvTables &) {
+        z = 0;                                         // frozen_lake.rs:107-108: the categorical
+        return 0u;                                     // draw returns 0 for every u: not drawn
     }
     template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
@@ -606,12 +608,9 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
         z += 1;
         const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
         uint32_t i = 0;
-        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {   // :126, drawn even when not slippery
+        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {   // :126 (a deterministic map's draw is unused: skipped)
             const double u = uniform01(r);
             if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
-        } else {
-            r.skip_u32();                              // deterministic map: the draw's value is unused
-            r.skip_u32();
         }
         const uint32_t o = (w >> (8 * i)) & 0xffu;
         s2 = o & 63u;
@@ -627,11 +626,9 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE> {
 // observes the current position with -1.0 (:227-231); one draw per step (:235).
 template <> struct EnvDev<RL_ENV_FROZEN_LAKE_EDITED> {
     static constexpr int A = 4;
-    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &r, const EnvTables &) {
-        r.skip_u32();                                  // :222-223, the start is position 0
-        r.skip_u32();                                  // (same maps as FrozenLakeEnv)
-        z = 0;
-        return 0u;
+    __device__ static __forceinline__ uint32_t reset(uint32_t &z, Rng &, const EnvTables &) {
+        z = 0;                                         // :222-223, the start is position 0
+        return 0u;                                     // (same maps as FrozenLakeEnv): not drawn
     }
     template <int SLIP = -1, bool AM = false>
     __device__ static __forceinline__ void step(uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
@@ -641,12 +638,9 @@ template <> struct EnvDev<RL_ENV_FROZEN_LAKE_EDITED> {
         z += 1;
         const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
         uint32_t i = 0;
-        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {
+        if (SLIP == 1 || (SLIP < 0 && t.slippery)) {   // :235 (skipped on a deterministic map)
             const double u = uniform01(r);
             if (w & (1u << 24)) i = (t.th1 > u) ? 0u : (t.th2 > u) ? 1u : (t.th3 > u) ? 2u : 0u;
-        } else {
-            r.skip_u32();
-            r.skip_u32();
         }
         const uint32_t o = (w >> (8 * i)) & 0xffu;
         s2 = o & 63u;

@@ -660,9 +660,10 @@ bool fix_proven(const rl_agent *a) { return delta_bound(a) < 2000.0; }
 // The 8-wave kernels pack a step's contributions to an entry into one int64,
 // sum * 2^11 + count (one LDS atomic per contribution instead of two): exact
 // while at most G contributions of at most delta_bound * 2^40 + 1 raw units each
-// keep |sum| * 2^11 + 2047 below 2^63, i.e. G * delta_bound < 2^12 (FrozenLake and
-// Blackjack at the CLI defaults: 0.15 * 512 and 2.0 * 512)
-bool pack_proven(const rl_agent *a) { return (double)a->G * delta_bound(a) < 4000.0; }
+// keep |sum| * 2^11 + 2047 below 2^63 — and |sum| below 2^51, so the settle converts
+// it with the 1.5*2^52 magic add: G * delta_bound < 2^11 (FrozenLake and Blackjack
+// at the CLI defaults: 0.15 * 512 and 2.0 * 512)
+bool pack_proven(const rl_agent *a) { return (double)a->G * delta_bound(a) < 2000.0; }
 
 // Write a freshly set table (P*S*A values) as the shared base: in the fixed point
 // when allowed (not forced to f64, the proof holds with Q0 = max |value|, every
@@ -720,6 +721,7 @@ int agent_recheck_repr(rl_agent *a) {
 void agent_sync_params(rl_agent *a) {
     KParams &p = a->kp;
     p.lr = a->cfg.lr;
+    p.lr40 = ldexp(a->cfg.lr, 40);
     p.gamma = a->cfg.gamma;
     p.gl = a->cfg.gamma * a->cfg.lambda;   // discount_factor * lambda_factor (elegibility_traces_agent.rs:94)
     p.eps_decay = a->cfg.eps_decay;

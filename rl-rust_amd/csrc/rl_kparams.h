@@ -100,6 +100,9 @@ struct KParams {
     double trunc_reward;
     // hyper-parameters
     double lr, gamma, gl, eps_decay, eps_final, ucb_c;
+    // lr * 2^40 (exact): the fixed point's rint(RN(lr * td) * 2^40) is rint(RN(lr40 * td))
+    // — scaling by 2^40 commutes with rounding; where lr * td is subnormal both are 0
+    double lr40;
     double eps_dm, eps_ds;     // decay as eps * dm - ds (rl_device.h decay_eps)
     int32_t decay_kind, algo;  // algo: informational (kernels are specialised on it)
     // fixed point only: the host proved that a step's contributions to an entry fit

@@ -29,8 +29,9 @@ size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint
                          uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack) {
     const int traces = agent != RL_AGENT_TRACES ? 0 : layout_sparse_traces(agent, sel, algo, 0) ? 2 : 1;
     const int ucb = sel != RL_SEL_UCB ? 0 : algo == RL_ALGO_EXPECTED_SARSA ? 2 : 1;
-    return smem_layout(env, policy == RL_POLICY_DOUBLE ? 2 : 1, ucb, traces, S, A, n_start, nthr, trc_kb, fq,
-                       ucb_pack).total;
+    const int P = policy == RL_POLICY_DOUBLE ? 2 : 1;
+    return smem_layout(env, P, ucb, traces, S, A, n_start, nthr, trc_kb, fq, ucb_pack,
+                       qsh_layout(fq, ucb, P, algo) ? 1 : 0).total;
 }
 
 // ---------------------------------------------------------------- lane init

@@ -14,7 +14,9 @@ eps-greedy or UCB selection:
 
 thread_rng() is replaced, at the same draw sites, by the build's per-lane
 xoshiro128+ stream, with rand 0.8.5's Uniform<f64> and
-Uniform<usize> mappings.  Python floats are IEEE binary64 and the loop does
+Uniform<usize> mappings; the stream skips the draws whose values the reference
+never looks at (the one-'S' reset, a deterministic map's step, the low word of
+a power-of-two Uniform<usize>).  Python floats are IEEE binary64 and the loop does
 the reference's operations in the reference's order, so its results are the
 reference arithmetic bit for bit; ln() is CPython's math.log (the platform
 libm, like Rust's f64::ln).
@@ -62,6 +64,8 @@ class Xoshiro128p:
         return struct.unpack("<d", struct.pack("<Q", (self.u64() >> 12) | 0x3FF0000000000000))[0] - 1.0
 
     def uniform_usize(self, n):                   # rand UniformInt<usize>::sample
+        if n >= 2 and n & (n - 1) == 0:           # the top bits of the u64's high word only
+            return self.u32() >> (32 - (n.bit_length() - 1))
         zone = M64 - ((1 << 64) - n) % n      # u64::MAX - (u64::MAX - range + 1) % range
         while True:
             m = self.u64() * n
@@ -88,6 +92,7 @@ def categorical_sample(probs, u):
 
 class FrozenLake:
     def __init__(self, map8x8=False, slippery=False, max_steps=100):
+        self.slippery = slippery
         m = MAP8 if map8x8 else MAP4
         n = len(m)
         self.n = n
@@ -129,7 +134,8 @@ class FrozenLake:
         self.curr_step = 0
 
     def reset(self, rng):
-        self.pos = categorical_sample(self.start, rng.uniform01())
+        fixed = sum(1 for x in self.start if x != 0.0) == 1   # one 'S': the same state for every u
+        self.pos = categorical_sample(self.start, 0.0 if fixed else rng.uniform01())
         self.ready = True
         self.curr_step = 0
         return self.pos
@@ -142,7 +148,7 @@ class FrozenLake:
             return 0, 0.0, True
         self.curr_step += 1
         tr = self.probs[self.pos][a]
-        i = categorical_sample([t[0] for t in tr], rng.uniform01())
+        i = categorical_sample([t[0] for t in tr], rng.uniform01()) if self.slippery else 0
         _, s, r, t = tr[i]
         self.pos = s
         if t:
