@@ -18,8 +18,13 @@
 
 namespace rlamd {
 
+#ifndef RLAMD_FUSE_MAX
+#define RLAMD_FUSE_MAX 2   // single-table Q-learning: one argmax+max pass per step (0: off,
+                           // 1: fused, 2: fused and pinned before the selection)
+#endif
+
 struct SmemLayout {
-    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, total;
+    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, qd, total;
     uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
@@ -51,6 +56,17 @@ __host__ __device__ inline uint32_t bj_dense(uint32_t row) {      // LDS row -> 
 __host__ __device__ constexpr bool pair_pool_env(int env) {
     return env == RL_ENV_CLIFF_WALKING || env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED;
 }
+// Fixed-point single-table Q-learning (rl_device.h argmax_max, the fused argmax +
+// max of the target row) keeps an f64 image of every entry beside its int64 word:
+// the step reads values (selection, TD target, Q(s,a)) without converting, and
+// the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_QSH
+#define RLAMD_QSH 2   // 0: off; 1: row reads as the compiler picks (ds_read2_b64: 0.2574 ms on cfg 2);
+                      // 2: rows as 16-byte reads (0.2156 ms; no shadow 0.2206 ms)
+#endif
+__host__ __device__ constexpr bool qsh_layout(int fq, int ucb, int P, int algo) {
+    return RLAMD_QSH && RLAMD_FUSE_MAX && !fq && !ucb && P == 1 && algo == RL_ALGO_QLEARNING;
+}
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   misc u32[4]            f64 traces: the group step's max td code
 //   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40, or f64 bits)
@@ -75,7 +91,8 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // counts u16 [S][A], or both in one u32 when ucb_pack)
 __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int traces, uint32_t S,
                                                   uint32_t A, uint32_t n_start, uint32_t nthr,
-                                                  uint32_t trc_kb = 40u, int fq = 0, int ucb_pack = 0) {
+                                                  uint32_t trc_kb = 40u, int fq = 0, int ucb_pack = 0,
+                                                  int qsh = 0) {
     const int shared_q = nthr != 0;
     SmemLayout l;
     const uint32_t SL = (shared_q && bj_compact(env, ucb)) ? BJ_LDS_STATES : S;   // LDS rows
@@ -123,6 +140,10 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     l.trc = off;
     if (pool) off += l.trc_cap ? align16(l.trc_cap * (nthr >> 6) * 2u) + l.trc_cap * (nthr >> 6) * 8u : 0u;
     else off += l.trc_cap ? align16(l.trc_cap * (nthr + 2u) * 2u) + l.trc_cap * (nthr + 1u) * 8u : 0u;
+    // qd  f64 [P][S][A]  fixed-point single-table Q-learning: the f64 image of every
+    //                    entry beside its int64 word (qsh_layout), read by the step
+    if (shared_q && qsh) off = align16(off);
+    l.qd = off; off += (shared_q && qsh) ? PSA * 8u : 0u;
     l.total = off;
     return l;
 }
@@ -354,10 +375,7 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // the 8-wave kernel), so off
 #define RLAMD_BJ_ONE_LOOP 0
 #endif
-#ifndef RLAMD_FUSE_MAX
-#define RLAMD_FUSE_MAX 2   // single-table Q-learning: one argmax+max pass per step (0: off,
-                           // 1: fused, 2: fused and pinned before the selection)
-#endif
+
 #ifndef RLAMD_SWEEP_U
 #define RLAMD_SWEEP_U 4   // pair-trace sweep: rounds of 64 items interleaved per iteration
                           // (cfg 4: 1 / 2 / 4 -> 1.163 / 1.089 / 1.058 ms per launch)
@@ -554,9 +572,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t tid = threadIdx.x, nthr = blockDim.x;
     constexpr bool PAIRS = TRACES && !SPEC;            // layout_sparse_traces (rl_kparams.h)
+    constexpr bool QSH = qsh_layout(FQ ? 1 : 0, UCB ? 1 : 0, P, ALGO);
     const SmemLayout lay = smem_layout(ENV, P, UCB ? (SPEC ? 2 : 1) : 0, TRACES ? (PAIRS ? 2 : 1) : 0, S, A, p.n_start,
-                                       nthr, p.trc_kb, FQ ? 1 : 0, p.ucb_pack);
+                                       nthr, p.trc_kb, FQ ? 1 : 0, p.ucb_pack, QSH ? 1 : 0);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
+    double *QD = (double *)(smem + lay.qd);              // QSH: f64 images of Q's words
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // fixed point: two u16 counters per word
     uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
@@ -608,7 +628,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if (tid < STATS_W) ACC[tid] = 0ull;
     if (tid == 0) GCODE[0] = 0u;
     for (uint32_t i = tid; i < lay.nrcp; i += nthr) RCP[i] = i == 0 ? 0.0 : 1.0 / (double)i;
-    for (uint32_t j = tid; j < PSAL; j += nthr) { Q[j] = (unsigned long long)p.q_base[dense_of(j)]; SUM[j] = 0ull; }
+    for (uint32_t j = tid; j < PSAL; j += nthr) {
+        Q[j] = (unsigned long long)p.q_base[dense_of(j)];
+        SUM[j] = 0ull;
+        if constexpr (QSH) QD[j] = q_val((int64_t)Q[j]);
+    }
     if constexpr (FQ && !TRACES) {
         for (uint32_t j = tid; j < PSAL; j += nthr) W[j] = 0u;
     } else {
@@ -768,6 +792,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (FQ) return as_f64((uint64_t)raw);
         else return q_val(raw);
     };
+    // QSH: the f64 images of row s; an A == 4 row (32 bytes, 16-aligned) as two
+    // 16-byte reads (element-wise, the compiler issued ds_read2_b64: 19 % slower on cfg 2)
+    auto qd_row = [&](uint32_t s, double (&v)[A]) {
+        if constexpr (A == 4 && RLAMD_QSH == 2) {
+            const double2 *r2 = (const double2 *)__builtin_assume_aligned(QD + qi(0, s, 0), 16);
+            const double2 x = r2[0], y = r2[1];
+            v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+        } else {
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = QD[qi(0, s, i)];
+        }
+    };
     // raw rows of state s: table 0 and (double policy) table 1, read once per use
     auto load_rows = [&](uint32_t s, int64_t (&ra)[A], int64_t (&rb)[A]) {
         if constexpr (BJC) {
@@ -866,7 +902,14 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[idx];
         const int64_t sum = PACKC ? (packed >> 11) : packed;
         const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
-        Q[idx] = Q[idx] + (unsigned long long)mean_delta_rcp(sum, rc);
+        // packed: |sum| < 2^51 (pack_proven), so (double)sum is the 1.5*2^52 magic
+        const double sd = PACKC ? __longlong_as_double((long long)(0x4338000000000000ull + (uint64_t)sum)) - 0x1.8p52
+                                : (double)sum;
+        const double y = __builtin_trunc(sd * rc) + 0x1.8p52;   // mean_delta_rcp
+        const int64_t md = (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
+        const unsigned long long q = Q[idx] + (unsigned long long)md;
+        Q[idx] = q;
+        if constexpr (QSH) QD[idx] = q_val((int64_t)q);
         SUM[idx] = 0ull;
         if constexpr (!PACKC) CNT16[idx] = 0;
     };
@@ -895,7 +938,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // one atomic per visited state instead of A.  Row sweep when every row has a
     // thread, else the first contributor of a row lists it.
     uint32_t *const CNTR = CNT;
-    const bool rsweep = (uint32_t)P * SL <= nthr;
+    // row sweep: every row settled by a strided pass (rows with no count return at
+    // once), so a visit's count needs no return value.  Pair pools (small tables,
+    // P * S <= 128 rows) always sweep: the list form's returning atomic made every
+    // first-of-state item wait for all of the wave's outstanding LDS operations
+    const bool rsweep = POOL || (uint32_t)P * SL <= nthr;
     auto qi_row = [&](uint32_t tbl, uint32_t row, uint32_t a) -> uint32_t {
         return LDS_AM ? tbl * SAL + a * SL + row : tbl * SAL + row * (uint32_t)A + a;
     };
@@ -960,6 +1007,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
                             for (int i = 0; i < A; ++i) v[i] = as_f64(ra2[i]);
                             pre = (int32_t)argmax_max_f64<A>(v, m);
+                        } else if constexpr (QSH) {
+                            double v[A], m;
+                            qd_row(s0, v);
+                            pre = (int32_t)argmax_max_f64<A>(v, m);
                         } else {
                             pre = (int32_t)argmax_i64<A>(ra2);
                         }
@@ -1018,6 +1069,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 double v[A];
 #pragma unroll
                 for (int i = 0; i < A; ++i) v[i] = as_f64(ra2[i]);
+                rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
+                if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
+            } else if constexpr (QSH) {
+                double v[A];
+                qd_row(s2, v);
                 rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
                 if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
             } else {
@@ -1090,6 +1146,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         for (int i = 0; i < A; ++i) v[i] = as_f64(rv[i]);
                         fq = vmax<A>(v);                   // utils::max
                     }
+                } else if constexpr (QSH) {
+                    fq = rmaxd;                            // the f64 image's max (exact)
                 } else {
                     fq = q_val(FUSE_MAX ? rmax : max_i64<A>(rv));   // utils::max on exact images
                 }
@@ -1132,7 +1190,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 td = __builtin_nan("");                    // r + gamma * NaN - q
             } else {
                 const uint32_t qidx = qi(vt, L.s, L.a);
-                const double qa = val((int64_t)Q[qidx]);
+                const double qa = QSH ? QD[qidx] : val((int64_t)Q[qidx]);
                 td = r + p.gamma * fq - qa;
             }
         }
@@ -1167,7 +1225,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 else if (owner) settle_fq(idx);
             } else {
                 bool owner = false;
-                if (train) owner = contribute(idx, q_fix_inrange(p.lr * td), 1u);
+                if (train) owner = contribute(idx, rint_i64_small(p.lr40 * td), 1u);   // q_fix_inrange(lr * td)
                 __syncthreads();   // all contributions in, all Q reads done
                 if (sweep) { if (tid < PSAL) settle(tid); }
                 else if (owner) settle(idx);
@@ -1207,8 +1265,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         pbits_set(id);
                     }
                 }
-                const uint64_t trM = __ballot(train), tmM = __ballot(train && term);
-                const uint32_t pk = hid | (ut << 16);
+                // shuffled to the lane's items with its td: the E += 1 pair (bits 0-8),
+                // the update table (16), "trains this step" (20), "its episode ends" (21)
+                const uint32_t pk = hid | (ut << 16) | (train ? 1u << 20 : 0u) | (train && term ? 1u << 21 : 0u);
                 const uint32_t C = lay.trc_cap;
                 const uint64_t below = (1ull << plid) - 1ull;
                 uint32_t wpos = 0;                             // items kept so far (uniform)
@@ -1246,13 +1305,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
-                        const uint32_t q = q0 + 64u * u + plid, il = (tg[u] >> 8) & 63u;
+                        const uint32_t q = q0 + 64u * u + plid;
                         const bool valid = q < npool;
-                        const bool istr = valid && ((trM >> il) & 1ull);
-                        const bool keep = valid && !((tmM >> il) & 1ull);
+                        const bool istr = valid && ((pkv[u] >> 20) & 1u);
+                        const bool keep = valid && !((pkv[u] >> 21) & 1u);
                         double en = ev[u];
                         if (istr) {
-                            const uint32_t id = tg[u] & 0xffu, uto = pkv[u] >> 16;
+                            const uint32_t id = tg[u] & 0xffu, uto = P == 2 ? (pkv[u] >> 16) & 1u : 0u;
                             const double e1 = id == (pkv[u] & 0x1ffu) ? ev[u] + 1.0 : ev[u];
                             const uint32_t o = id >> 2, b = id & 3u;   // A == 4
                             if (tg[u] & 0x8000u) {
@@ -1496,7 +1555,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             __syncthreads();   // all contributions in, all Q reads done
             if (tid == 0) GCODE[0] = 0u;                  // read by every thread before the sweep
             if (rsweep) {
-                if (tid < (uint32_t)P * SL) settle_row(tid, e_tr);
+                for (uint32_t r = tid; r < (uint32_t)P * SL; r += nthr) settle_row(r, e_tr);
             } else {
                 const uint32_t n_touched = LISTN[0];
                 for (uint32_t i = tid; i < n_touched; i += nthr) settle_row(LIST[i], e_tr);
