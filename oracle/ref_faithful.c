@@ -39,7 +39,8 @@
  * oracle's per-lane xoshiro128+ stream (which also skips the
  * draws whose values the reference never looks at: FrozenLake's reset and
  * deterministic-map step draws, and the low word of a power-of-two action
- * draw) and libm's ln by the
+ * draw, Blackjack's cards two per word, the eps test's low word when the high
+ * word decides it) and libm's ln by the
  * oracle's fdlibm one (a last-ulp difference at some t reaches UCB + expected
  * SARSA's probabilities): the run is then bit-identical to
  * oracle/rlref.c's rlo_faithful loop, which tests/test_oracle_cross.py checks —
@@ -129,6 +130,18 @@ static inline double unif01(rng_t *r) {
     union { uint64_t u; double d; } b = {(rng_u64(r) >> 12) | 0x3FF0000000000000ull};
     return b.d - 1.0;
 }
+#ifdef RF_XOSHIRO
+/* the oracle's stream: the eps test draws m's top 32 bits first, the low word
+ * only when they leave it undecided (rlref.c eps_test) */
+static inline int eps_test_xo(rng_t *r, double eps) {
+    const uint32_t h = rng_u32(r);
+    const double e32 = ldexp(eps, 32), hd = (double)h;
+    if (hd + 1.0 <= e32) return 1;
+    if (!(hd < e32)) return 0;
+    union { uint64_t u; double d; } b = {((((uint64_t)h << 32) | rng_u32(r)) >> 12) | 0x3FF0000000000000ull};
+    return b.d - 1.0 < eps;
+}
+#endif
 static inline uint32_t unif_action(rng_t *r, uint32_t n) {
 #ifdef RF_XOSHIRO
     /* the oracle's stream: a power-of-two range takes one u32's top bits (the
@@ -255,16 +268,31 @@ static void inc(int nrow, int ncol, int row, int col, int a, int *nr, int *nc) {
     else if (a == 2) *nc = col + 1 < ncol ? col + 1 : ncol - 1;
     else if (a == 3) *nr = row ? row - 1 : 0;
 }
-static uint8_t draw_card(rng_t *g) {              /* rand 0.8.5 Uniform<u8>(1..11): u32 widening, zone */
+typedef struct { uint32_t w, n; } cards_t;   /* RF_XOSHIRO: the env operation's word, halves left */
+static uint8_t draw_card(rng_t *g, cards_t *cs) {   /* rand 0.8.5 Uniform<u8>(1..11): u32 widening, zone */
+#ifdef RF_XOSHIRO
+    /* the oracle's stream: the same rule on 16-bit halves, two cards per word,
+     * per env operation (rlref.c cardsrc) */
+    for (;;) {
+        if (cs->n == 0) { cs->w = rng_u32(g); cs->n = 2; }
+        const uint32_t h = cs->n == 2 ? cs->w >> 16 : cs->w & 0xFFFFu;
+        cs->n--;
+        const uint32_t m = h * 10u;
+        if ((m & 0xFFFFu) <= 0xFFFFu - 6u) return (uint8_t)(1u + (m >> 16));
+    }
+#else
+    (void)cs;
     const uint32_t zone = 0xFFFFFFFFu - 6u;
     for (;;) {
         const uint64_t m = (uint64_t)rng_u32(g) * 10u;
         if ((uint32_t)m <= zone) return (uint8_t)(1u + (uint32_t)(m >> 32));
     }
+#endif
 }
 static void bj_init_hands(env_t *e, rng_t *g) {                                            /* blackjack.rs:60-69 */
-    e->player[0] = draw_card(g); e->player[1] = draw_card(g); e->pi = 2;
-    e->dealer[0] = draw_card(g); e->dealer[1] = draw_card(g); e->di = 2;
+    cards_t cs = {0, 0};
+    e->player[0] = draw_card(g, &cs); e->player[1] = draw_card(g, &cs); e->pi = 2;
+    e->dealer[0] = draw_card(g, &cs); e->dealer[1] = draw_card(g, &cs); e->di = 2;
     e->pace = e->player[0] == 1 || e->player[1] == 1;
     e->dace = e->dealer[0] == 1 || e->dealer[1] == 1;
 }
@@ -410,8 +438,9 @@ static uint64_t env_reset(env_t *e, rng_t *g) {
 static int env_step(env_t *e, uint32_t a, rng_t *g, uint64_t *s2, double *r, int *term) {
     if (!e->ready) return -1;
     if (e->kind == ENV_BJ) {                                                                  /* blackjack.rs:118-163 */
+        cards_t cs = {0, 0};
         if (a == 0) {
-            e->player[e->pi++] = draw_card(g);
+            e->player[e->pi++] = draw_card(g, &cs);
             const uint8_t p = hand_score(e->player, e->pace);
             if (p > 21) {
                 e->ready = 0;
@@ -424,7 +453,7 @@ static int env_step(env_t *e, uint32_t a, rng_t *g, uint64_t *s2, double *r, int
         e->ready = 0;
         uint8_t d = hand_score(e->dealer, e->dace);
         while (d < 17) {
-            e->dealer[e->di++] = draw_card(g);
+            e->dealer[e->di++] = draw_card(g, &cs);
             d = hand_score(e->dealer, e->dace);
         }
         const uint8_t p = hand_score(e->player, e->pace);
@@ -519,7 +548,11 @@ static uint32_t get_action(agent_t *ag, uint64_t s) {                           
     double v[MAXA];
     predict(ag, s, v);
     if (!ag->ucb) {                                                                       /* uniform_epsilon_greed.rs:51-66 */
+#ifdef RF_XOSHIRO
+        if (ag->eps != 0.0 && eps_test_xo(ag->g, ag->eps)) return unif_action(ag->g, ag->A);
+#else
         if (ag->eps != 0.0 && unif01(ag->g) < ag->eps) return unif_action(ag->g, ag->A);
+#endif
         return argmax_a(v, ag->A);
     }
     u128 *cnt = (u128 *)map_entry(&ag->n, s, CZERO);

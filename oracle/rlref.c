@@ -306,6 +306,26 @@ double rlo_u64_to_uniform01(uint64_t bits) {
 }
 static inline double uniform01(rlo_rng *r) { return rlo_u64_to_uniform01(next_u64(r)); }
 
+/* eps-greedy's test u < eps, u = UniformFloat(0..1) = m * 2^-52 with m the top 52
+ * bits of a u64 (uniform_epsilon_greed.rs:51-54): the stream draws m's top 32 bits
+ * h first; they decide unless h*2^-32 < eps < (h+1)*2^-32, and only then is the
+ * word holding m's low 20 bits drawn — the same exact test (DESIGN.md §2 "draws";
+ * device: rl_device.h eps_test). */
+int rlo_eps_test_words(uint32_t h, uint32_t l, double eps, int *need_low) {
+    const double e32 = ldexp(eps, 32), hd = (double)h;
+    *need_low = 0;
+    if (hd + 1.0 <= e32) return 1;
+    if (!(hd < e32)) return 0;
+    *need_low = 1;
+    return rlo_u64_to_uniform01(((uint64_t)h << 32) | l) < eps;
+}
+static int eps_test(rlo_rng *r, double eps) {
+    const uint32_t h = next_u32(r);
+    int need;
+    int lt = rlo_eps_test_words(h, 0, eps, &need);
+    if (need) lt = rlo_eps_test_words(h, next_u32(r), eps, &need);
+    return lt;
+}
 /* rand 0.8.5 UniformInt<usize>::sample (widening multiply + rejection zone),
  * for Uniform::from(0..COUNT) (uniform_epsilon_greed.rs:34,62). */
 uint32_t rlo_uniform_int_u64(uint64_t v, uint64_t range, int *reject) {
@@ -375,10 +395,25 @@ uint32_t rlo_uniform_card_u32(uint32_t v, int *reject) {
     *reject = !(lo <= zone);
     return 1u + hi;
 }
-static uint32_t draw_card(rlo_rng *r) {
+/* The stream's cards (DESIGN.md §2 "cards"): the same widening-multiply-and-zone
+ * rule on 16-bit halves — card 1 + (h*10 >> 16), rejected when (h*10 & 0xffff) >
+ * 65535 - (2^16 % 10) — an exact uniform over 1..10 as the u32 rule is, so one u32
+ * supplies two cards, high half first.  Each env operation (a deal, a hit, the
+ * dealer's draws after a stick) takes its cards from its own words (cardsrc): a
+ * rejected half is skipped, a half left at the operation's end is discarded. */
+uint32_t rlo_uniform_card_u16(uint32_t h, int *reject) {
+    const uint32_t m = (h & 0xFFFFu) * 10u;
+    *reject = !((m & 0xFFFFu) <= 0xFFFFu - 6u);
+    return 1u + (m >> 16);
+}
+typedef struct { uint32_t w, n; } cardsrc;   /* the operation's current word, halves left */
+static uint32_t draw_card(rlo_rng *r, cardsrc *cs) {
     for (;;) {
+        if (cs->n == 0) { cs->w = next_u32(r); cs->n = 2; }
+        const uint32_t h = cs->n == 2 ? cs->w >> 16 : cs->w & 0xFFFFu;
+        cs->n--;
         int rej;
-        uint32_t c = rlo_uniform_card_u32(next_u32(r), &rej);
+        uint32_t c = rlo_uniform_card_u16(h, &rej);
         if (!rej) return c;
     }
 }
@@ -683,7 +718,8 @@ static inline uint32_t bj_score(uint32_t sum, uint32_t ace) { return (ace && sum
 /* dense obs index: p_score <= 31, d_score <= 26 (dealer stops at >= 17) */
 static inline uint32_t bj_index(uint32_t p, uint32_t d, uint32_t ace) { return (p * 32 + d) * 2 + (ace ? 1 : 0); }
 static void bj_initialize_hands(envstate *st, rlo_rng *r) {       /* :47-56 */
-    uint32_t p0 = draw_card(r), p1 = draw_card(r), d0 = draw_card(r), d1 = draw_card(r);
+    cardsrc cs = {0, 0};
+    uint32_t p0 = draw_card(r, &cs), p1 = draw_card(r, &cs), d0 = draw_card(r, &cs), d1 = draw_card(r, &cs);
     st->p_sum = p0 + p1; st->d_sum = d0 + d1; st->d0 = d0;
     st->p_ace = p0 == 1 || p1 == 1;
     st->d_ace = d0 == 1 || d1 == 1;
@@ -718,7 +754,8 @@ static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint3
     if (!st->ready) return -1;
     if (E->kind == RLO_ENV_BLACKJACK) {
         if (a == 0) {                                   /* hit :121-138 */
-            st->p_sum += draw_card(r);
+            cardsrc cs = {0, 0};
+            st->p_sum += draw_card(r, &cs);
             uint32_t p = bj_score(st->p_sum, st->p_ace);
             if (p > 21) {
                 st->ready = 0;
@@ -732,8 +769,9 @@ static int env_step(const envdef *E, envstate *st, uint32_t a, rlo_rng *r, uint3
         }
         st->ready = 0;                                  /* stick :139-162 */
         uint32_t d = bj_score(st->d_sum, st->d_ace);
+        cardsrc cs = {0, 0};
         while (d < 17) {
-            st->d_sum += draw_card(r);
+            st->d_sum += draw_card(r, &cs);
             d = bj_score(st->d_sum, st->d_ace);
         }
         uint32_t p = bj_score(st->p_sum, st->p_ace);
@@ -1145,7 +1183,7 @@ static uint32_t f_get_action(rlo_faithful *f, uint32_t s) {
     double v[MAXA];
     f_predict(f, s, v);
     if (f->c.selector == RLO_SEL_EPS_GREEDY) {             /* uniform_epsilon_greed.rs:60-66 */
-        if (f->eps != 0.0 && uniform01(&f->rng) < f->eps) return uniform_action(&f->rng, f->A);
+        if (f->eps != 0.0 && eps_test(&f->rng, f->eps)) return uniform_action(&f->rng, f->A);
         return argmax_d(v, f->A);
     }
     uint64_t *n = &f->ucb_n[(size_t)s * f->A];             /* upper_confidence_bound.rs:29-42 */
@@ -1587,7 +1625,7 @@ static uint32_t b_select(rlo_batch *b, lane_t *L, uint32_t s) {
     double v[MAXA];
     b_predict(b, s, v);
     if (b->c.selector == RLO_SEL_EPS_GREEDY) {
-        if (L->eps != 0.0 && uniform01(&L->rng) < L->eps) return uniform_action(&L->rng, b->A);
+        if (L->eps != 0.0 && eps_test(&L->rng, L->eps)) return uniform_action(&L->rng, b->A);
         return argmax_d(v, b->A);
     }
     const uint64_t *n = &b->n_g[(size_t)s * b->A];

@@ -87,6 +87,8 @@ void     rlo_rng_stream(uint64_t seed, uint64_t lane, uint32_t n, uint32_t *out)
 double   rlo_u64_to_uniform01(uint64_t bits);       /* rand 0.8 UniformFloat<f64>(0..1) */
 uint32_t rlo_uniform_int_u64(uint64_t v, uint64_t range, int *reject);  /* rand 0.8 UniformInt<usize> */
 uint32_t rlo_uniform_card_u32(uint32_t v, int *reject);                 /* rand 0.8 Uniform<u8>(1..11) */
+uint32_t rlo_uniform_card_u16(uint32_t h, int *reject);                 /* the stream's card rule on a 16-bit half */
+int rlo_eps_test_words(uint32_t h, uint32_t l, double eps, int *need_low); /* the stream's eps test (l read only if *need_low) */
 uint64_t rlo_blackjack_obs_id(uint32_t p_score, uint32_t d_score, uint32_t p_ace); /* fxhash 0.2.1 */
 int      rlo_env_dims(const rlo_config *c, uint32_t *n_states, uint32_t *n_actions);
 /* transition table export: for each (s,a) up to 3 outcomes (prob, next, reward, term) */

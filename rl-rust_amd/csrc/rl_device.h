@@ -74,6 +74,31 @@ __device__ __forceinline__ double uniform01(Rng &r) {
     const uint64_t bits = (r.next_u64() >> 12) | 0x3FF0000000000000ull;
     return __longlong_as_double((long long)bits) - 1.0;
 }
+// The eps-greedy test u < eps for u = UniformFloat(0..1) = m * 2^-52, m the top 52
+// bits of a u64 (uniform_epsilon_greed.rs:51-54): the high word h is drawn first
+// and decides the test unless h * 2^-32 < eps < (h + 1) * 2^-32 (probability
+// <= 2^-32); only then is the word holding m's low 20 bits drawn (DESIGN §2
+// "draws": the same exact test, one u32 per selection).  eps * 2^32 and h + 1
+// are exact; NaN eps fails every compare and reaches the exact test.
+#ifndef RLAMD_EPSX
+#define RLAMD_EPSX 1
+#endif
+__device__ __forceinline__ bool eps_test(Rng &r, double eps) {
+    const uint32_t h = r.next_u32();
+    const double e32 = __builtin_ldexp(eps, 32), hd = (double)h;
+    bool lt = hd + 1.0 <= e32;                  // u < (h + 1) 2^-32 <= eps
+#if RLAMD_EPSX
+    const bool may = hd < e32;                  // u < eps possible (implied by lt)
+    if (may != lt) {                            // undecided: m's low bits
+#else
+    if (!lt && hd < e32) {                      // undecided: m's low bits
+#endif
+        const uint32_t l = r.next_u32();
+        const uint64_t bits = (((((uint64_t)h << 32) | l) >> 12)) | 0x3FF0000000000000ull;
+        lt = __longlong_as_double((long long)bits) - 1.0 < eps;
+    }
+    return lt;
+}
 // rand 0.8.5 UniformInt<usize>::sample for Uniform::from(0..A)
 // (uniform_epsilon_greed.rs:34,62): widening multiply, reject lo > zone.
 // A power of two (FrozenLake / CliffWalking 4, Blackjack 2): the zone rejects
@@ -102,14 +127,30 @@ __device__ __forceinline__ uint32_t gen_index(Rng &r, uint32_t n) {
         if (v * range <= zone) return (uint32_t)__umul64hi(v, range);
     }
 }
-// rand 0.8.5 UniformInt<u8>(1..11) with u32 large type (blackjack.rs:542,562)
-__device__ __forceinline__ uint32_t draw_card(Rng &r) {
-    constexpr uint32_t zone = 0xFFFFFFFFu - 6u;
-    for (;;) {
-        const uint64_t m = (uint64_t)r.next_u32() * 10u;
-        if ((uint32_t)m <= zone) return 1u + (uint32_t)(m >> 32);
-    }
+// Cards (blackjack.rs:54, rand 0.8.5 Uniform<u8>(1..11)): rand's widening-multiply-
+// and-zone rule at 16 bits — a half h gives card 1 + (h*10 >> 16), rejected when
+// (h*10 & 0xffff) > 65535 - 6 — the same exact uniform over 1..10 as the u32 rule,
+// so one u32 supplies two cards, high half first (a 24-bit multiply instead of a
+// 64-bit one).  Each env operation (a deal, a hit, the dealer's draws after a
+// stick) takes its cards from its own words: a rejected half is skipped, a half
+// left at the operation's end is discarded (DESIGN §2 "cards"; oracle cardsrc).
+__device__ __forceinline__ bool card16(uint32_t h, uint32_t &c) {
+    const uint32_t m = __umul24(h, 10u);
+    c = 1u + (m >> 16);
+    return (m & 0xFFFFu) <= 0xFFFFu - 6u;
 }
+struct CardSrc {
+    uint32_t w = 0, n = 0;   // the operation's current word, halves left
+    __device__ __forceinline__ uint32_t next(Rng &r) {
+        for (;;) {
+            if (n == 0u) { w = r.next_u32(); n = 2u; }
+            const uint32_t h = n == 2u ? w >> 16 : w & 0xFFFFu;
+            --n;
+            uint32_t c;
+            if (card16(h, c)) return c;
+        }
+    }
+};
 
 // ------------------------------------------------------------------ ln()
 // fdlibm e_log.c operation sequence; the oracle (oracle/rlref.c rlo_log)
@@ -713,18 +754,18 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         return ((p << 5) + d) * 2u + ace;   // dense index (p*32 + d)*2 + ace: shifts to decode
     }
     __device__ static __forceinline__ uint32_t deal(Rng &r) {    // initialize_hands :47-56
-        // four words drawn back to back: when none falls in the rejection zone
-        // (all but ~6e-9 of deals) they are the four sequential draw_card results;
-        // otherwise the deal is redrawn sequentially from the saved state
+        // two words, four halves: when none is rejected (all but ~4e-4 of deals)
+        // they are the deal's four cards; otherwise it is redrawn card by card from
+        // the saved state
         const Rng r0 = r;
-        const uint64_t m0 = (uint64_t)r.next_u32() * 10u, m1 = (uint64_t)r.next_u32() * 10u,
-                       m2 = (uint64_t)r.next_u32() * 10u, m3 = (uint64_t)r.next_u32() * 10u;
-        constexpr uint32_t zone = 0xFFFFFFFFu - 6u;
-        uint32_t p0 = 1u + (uint32_t)(m0 >> 32), p1 = 1u + (uint32_t)(m1 >> 32), d0 = 1u + (uint32_t)(m2 >> 32),
-                 d1 = 1u + (uint32_t)(m3 >> 32);
-        if ((uint32_t)m0 > zone || (uint32_t)m1 > zone || (uint32_t)m2 > zone || (uint32_t)m3 > zone) {
+        const uint32_t w0 = r.next_u32(), w1 = r.next_u32();
+        uint32_t p0, p1, d0, d1;
+        const bool k0 = card16(w0 >> 16, p0), k1 = card16(w0 & 0xFFFFu, p1), k2 = card16(w1 >> 16, d0),
+                   k3 = card16(w1 & 0xFFFFu, d1);
+        if (!(k0 && k1 && k2 && k3)) {
             r = r0;
-            p0 = draw_card(r); p1 = draw_card(r); d0 = draw_card(r); d1 = draw_card(r);
+            CardSrc cs;
+            p0 = cs.next(r); p1 = cs.next(r); d0 = cs.next(r); d1 = cs.next(r);
         }
         const uint32_t pa = (p0 == 1u || p1 == 1u), da = (d0 == 1u || d1 == 1u);
         return (p0 + p1) | ((d0 + d1) << 8) | (d0 << 16) | (pa << 20) | (da << 21);
@@ -741,7 +782,8 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         uint32_t ps = z & 0xffu, ds = (z >> 8) & 0xffu;
         const uint32_t d0 = (z >> 16) & 0xfu, pa = (z >> 20) & 1u, da = (z >> 21) & 1u;
         if (a == 0) {                                  // hit :121-138
-            ps += draw_card(r);
+            CardSrc cs;
+            ps += cs.next(r);
             const uint32_t p = score(ps, pa);
             if (p > 21u) {
                 s2 = obs(p, score(ds, da), pa); rew = -1.0; term = true;
@@ -750,9 +792,11 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
             }
         } else {                                       // stick :139-162
             uint32_t d = score(ds, da);
-            while (d < 17u) {
-                ds += draw_card(r);
-                d = score(ds, da);
+            while (d < 17u) {                          // two cards per word (CardSrc's order)
+                const uint32_t w = r.next_u32();
+                uint32_t c;
+                if (card16(w >> 16, c)) { ds += c; d = score(ds, da); }
+                if (d < 17u && card16(w & 0xFFFFu, c)) { ds += c; d = score(ds, da); }
             }
             const uint32_t p = score(ps, pa);
             s2 = obs(p, d, pa);
@@ -775,9 +819,10 @@ template <> struct EnvDev<RL_ENV_BLACKJACK> {
         if (doR) { ps = 0u; ds = 0u; d0 = 0u; pa = 0u; da = 0u; }
         const bool hit = doS && a == 0u, stick = doS && a != 0u;
         const uint32_t nfix = doR ? 4u : (hit ? 1u : 0u);
+        CardSrc cs;                                    // the lane's operation draws its own words
         for (uint32_t i = 0;; ++i) {
             if (!(i < nfix || (stick && score(ds, da) < 17u))) break;
-            const uint32_t c = draw_card(r);
+            const uint32_t c = cs.next(r);
             if (doR) {
                 if (i < 2u) { ps += c; pa |= c == 1u ? 1u : 0u; }
                 else { if (i == 2u) d0 = c; ds += c; da |= c == 1u ? 1u : 0u; }
@@ -838,6 +883,11 @@ __device__ __forceinline__ double decay_eps(const KParams &p, double eps) {
 }
 
 // ------------------------------------------------------------------ wave helpers
+// set bits of a wave mask below this lane (v_mbcnt_lo + v_mbcnt_hi: two VALU ops,
+// where popcount(m & ((1 << lane) - 1)) compiled to two ANDs and two counts)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

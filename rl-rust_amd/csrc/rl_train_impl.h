@@ -60,12 +60,16 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // max of the target row) keeps an f64 image of every entry beside its int64 word:
 // the step reads values (selection, TD target, Q(s,a)) without converting, and
 // the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_TAIL
+#define RLAMD_TAIL 0   // 1: the throughput kernels' end-of-step bookkeeping as one predicated
+                       // block (cfg 2: 0.2149-0.2157 ms against 0.2139-0.2145, A/B on one box)
+#endif
 #ifndef RLAMD_QSH
 #define RLAMD_QSH 2   // 0: off; 1: row reads as the compiler picks (ds_read2_b64: 0.2574 ms on cfg 2);
                       // 2: rows as 16-byte reads (0.2156 ms; no shadow 0.2206 ms)
 #endif
 __host__ __device__ constexpr bool qsh_layout(int fq, int ucb, int P, int algo) {
-    return RLAMD_QSH && RLAMD_FUSE_MAX && !fq && !ucb && P == 1 && algo == RL_ALGO_QLEARNING;
+    return RLAMD_QSH != 0 && RLAMD_FUSE_MAX != 0 && !fq && !ucb && P == 1 && algo == RL_ALGO_QLEARNING;
 }
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   misc u32[4]            f64 traces: the group step's max td code
@@ -840,7 +844,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (!UCB) {                       // uniform_epsilon_greed.rs:51-66
             // one compare decides both the draw (skipped when eps == 0) and the branch
             bool explore = L.eps != 0.0;
-            if (explore) explore = uniform01(L.rng) < L.eps;
+            if (explore) explore = eps_test(L.rng, L.eps);
             if (explore) return uniform_action<A>(L.rng);
             if constexpr (FUSE_MAX) return (uint32_t)pre;
             if constexpr (FQ) {                     // argmax of predict(): (a + b) / 2.0 (double_tabular_policy.rs:31-39)
@@ -1269,7 +1273,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 // the update table (16), "trains this step" (20), "its episode ends" (21)
                 const uint32_t pk = hid | (ut << 16) | (train ? 1u << 20 : 0u) | (train && term ? 1u << 21 : 0u);
                 const uint32_t C = lay.trc_cap;
-                const uint64_t below = (1ull << plid) - 1ull;
                 uint32_t wpos = 0;                             // items kept so far (uniform)
                 constexpr uint32_t U = RLAMD_SWEEP_U;
                 for (uint32_t q0 = 0; q0 < npool; q0 += 64u * U) {
@@ -1322,7 +1325,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             en = e1 * p.gl;
                         }
                         const uint64_t m = __ballot(keep);
-                        const uint32_t pos = wpos + (uint32_t)__popcll(m & below);
+                        const uint32_t pos = wpos + lanes_below(m);
                         if (keep) {
                             if (wpos + 64u <= C || pos < C) { PT[pos] = (uint16_t)tg[u]; PE[pos] = en; }
                             else { HT[pos] = (uint16_t)tg[u]; HE[pos] = en; }
@@ -1340,7 +1343,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 const bool keepn = newp && !term;
                 const uint64_t m = __ballot(keepn);
                 if (keepn) {
-                    const uint32_t pos = wpos + (uint32_t)__popcll(m & below);
+                    const uint32_t pos = wpos + lanes_below(m);
                     const uint16_t tag = (uint16_t)(nid | (plid << 8) | (first_new ? 0x8000u : 0u));
                     const double en = 1.0 * p.gl;
                     if (pos < C) { PT[pos] = tag; PE[pos] = en; }
@@ -1577,7 +1580,33 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         }
         __syncthreads();   // Q_{t+1} complete before the next step's reads
         bool tr = false, ev = false;
-        if (doS) {
+        if constexpr (!INSTR && RLAMD_TAIL) {
+            // one predicated block (no STEP / RESET branches): the STEP lanes'
+            // bookkeeping computed for every lane, then every lane-state field written
+            // once by a select — RESET lanes start an episode, idle lanes keep theirs
+            if (train) {
+                if (P == 2) L.dflag = !L.dflag;            // after_update
+                if constexpr (!UCB) {                      // decay_epsilon: one select per lane
+                    const double nw = L.eps * p.eps_dm - p.eps_ds;
+                    L.eps = (term && !(p.eps_final > nw)) ? nw : L.eps;
+                }
+            }
+            LaneRegs N = L;
+            after_step(p, N, s2, a2, r, term, tr, ev);   // term is false on RESET / idle lanes
+            const bool act = doS || doR;
+            L.epi_reward = doS ? N.epi_reward : (doR ? 0.0 : L.epi_reward);
+            L.epi_len = doS ? N.epi_len : (doR ? 0u : L.epi_len);
+            L.s = act ? s2 : L.s;
+            L.a = act ? a2 : L.a;
+            L.train_ep = doS ? N.train_ep : L.train_ep;
+            L.mode = doS ? N.mode : L.mode;
+            L.eval_left = doS ? N.eval_left : L.eval_left;
+            L.need_reset = doS ? N.need_reset : (doR ? false : L.need_reset);
+            tr = tr && doS;
+            ev = ev && doS;
+            if (tr) atomicAdd(RSUM, (unsigned long long)(FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
+                                                             : rint_i64_small(L.epi_reward * 65536.0)));
+        } else if (doS) {
             if (train) {
                 if (P == 2) L.dflag = !L.dflag;            // after_update
                 if constexpr (!UCB) {                      // decay_epsilon: one select per lane
@@ -1840,7 +1869,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         double v[A];
         predict(s, v);
         if constexpr (!UCB) {
-            if (L.eps != 0.0 && uniform01(L.rng) < L.eps) return uniform_action<A>(L.rng);
+            if (L.eps != 0.0 && eps_test(L.rng, L.eps)) return uniform_action<A>(L.rng);
             return argmax<A>(v);
         } else {
             const double lnt = rl_log((double)t);

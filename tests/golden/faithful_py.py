@@ -16,7 +16,7 @@ thread_rng() is replaced, at the same draw sites, by the build's per-lane
 xoshiro128+ stream, with rand 0.8.5's Uniform<f64> and
 Uniform<usize> mappings; the stream skips the draws whose values the reference
 never looks at (the one-'S' reset, a deterministic map's step, the low word of
-a power-of-two Uniform<usize>).  Python floats are IEEE binary64 and the loop does
+a power-of-two Uniform<usize>), and draws the eps test's high word first.  Python floats are IEEE binary64 and the loop does
 the reference's operations in the reference's order, so its results are the
 reference arithmetic bit for bit; ln() is CPython's math.log (the platform
 libm, like Rust's f64::ln).
@@ -62,6 +62,16 @@ class Xoshiro128p:
 
     def uniform01(self):                          # rand UniformFloat<f64>, 0..1
         return struct.unpack("<d", struct.pack("<Q", (self.u64() >> 12) | 0x3FF0000000000000))[0] - 1.0
+
+    def eps_test(self, eps):                      # u < eps, m's top 32 bits drawn first
+        h = self.u32()
+        e32 = math.ldexp(eps, 32)
+        if h + 1.0 <= e32:
+            return True
+        if not h < e32:
+            return False
+        m = ((h << 32) | self.u32()) >> 12
+        return struct.unpack("<d", struct.pack("<Q", m | 0x3FF0000000000000))[0] - 1.0 < eps
 
     def uniform_usize(self, n):                   # rand UniformInt<usize>::sample
         if n >= 2 and n & (n - 1) == 0:           # the top bits of the u64's high word only
@@ -175,7 +185,7 @@ class Agent:
     def get_action(self, s):
         v = self.values(s)
         if self.sel == "eps_greedy":
-            if self.eps != 0.0 and self.rng.uniform01() < self.eps:
+            if self.eps != 0.0 and self.rng.eps_test(self.eps):
                 return self.rng.uniform_usize(self.A)
             return argmax(v)
         cnt, u = self._ucbs(s, v)

@@ -69,8 +69,9 @@ def run(job):
     return name, mode, kw, out
 
 
-def generate(workers=8):
-    jobs = [(n, "auto") for n in CASES] + [("cfg2", "f64")] + [(n, "f64_seq") for n in CASES[1:]]
+def generate(workers=8, only=None, old=None):
+    cases = [n for n in CASES if only is None or n in only]
+    jobs = [(n, "auto") for n in cases] + [(n, "f64" if n == "cfg2" else "f64_seq") for n in cases]
     with ProcessPoolExecutor(max_workers=workers) as ex:
         res = list(ex.map(run, jobs))
     main = {n: (kw, o) for n, m, kw, o in res if m == "auto"}
@@ -78,6 +79,9 @@ def generate(workers=8):
     doc = {"source": "tests/golden/make_horizon.py (oracle/rlref.c batched schedule, seed 0x5EED)",
            "n_episodes": N_EPISODES, "eval_at": N_EPISODES // 10}
     for n in CASES:
+        if n not in main:
+            doc[n] = old[n]
+            continue
         kw, o = main[n]
         q = o["q"]
         fin = np.isfinite(q)
@@ -104,6 +108,9 @@ def generate(workers=8):
 
 
 if __name__ == "__main__":
+    # python make_horizon.py [cfgN ...]: regenerate only these cases, keep the others
     path = os.path.join(HERE, "horizon.json")
-    json.dump(generate(), open(path, "w"), indent=1)
+    only = sys.argv[1:] or None
+    old = json.load(open(path)) if only else None
+    json.dump(generate(only=only, old=old), open(path, "w"), indent=1)
     print("wrote", path, os.path.getsize(path), "bytes")

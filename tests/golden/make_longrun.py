@@ -78,14 +78,18 @@ def case(name):
     return name, out
 
 
-def generate(workers=3):
+def generate(workers=3, only=None, old=None):
+    names = [k for k in LAUNCHES if only is None or k in only]
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        res = dict(ex.map(case, list(LAUNCHES)))
+        res = dict(ex.map(case, names))
     return {"source": "tests/golden/make_longrun.py (oracle/rlref.c batched schedule, seed 0x5EED)",
-            **{k: res[k] for k in LAUNCHES}}
+            **{k: res[k] if k in res else old[k] for k in LAUNCHES}}
 
 
 if __name__ == "__main__":
+    # python make_longrun.py [cfgN ...]: regenerate only these cases, keep the others
     path = os.path.join(HERE, "longrun.json")
-    json.dump(generate(), open(path, "w"), indent=1)
+    only = sys.argv[1:] or None
+    old = json.load(open(path)) if only else None
+    json.dump(generate(only=only, old=old), open(path, "w"), indent=1)
     print("wrote", path, os.path.getsize(path), "bytes")

@@ -115,6 +115,10 @@ def lib():
         L.rlo_batch_set_planning.argtypes = [C.c_void_p, C.c_uint32]
         L.rlo_uniform_card_u32.restype = C.c_uint32
         L.rlo_uniform_card_u32.argtypes = [C.c_uint32, P(C.c_int)]
+        L.rlo_uniform_card_u16.restype = C.c_uint32
+        L.rlo_eps_test_words.restype = C.c_int
+        L.rlo_eps_test_words.argtypes = [C.c_uint32, C.c_uint32, C.c_double, P(C.c_int)]
+        L.rlo_uniform_card_u16.argtypes = [C.c_uint32, P(C.c_int)]
         L.rlo_blackjack_obs_id.restype = C.c_uint64
         L.rlo_blackjack_obs_id.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
         L.rlo_env_dims.argtypes = [P(Config), P(C.c_uint32), P(C.c_uint32)]

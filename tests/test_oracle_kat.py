@@ -96,6 +96,37 @@ def test_kat_constants(oracle):
     assert L.rlo_uniform_card_u32(0xFFFFFFFF, ctypes.byref(rej)) == 10 and rej.value == 0
     L.rlo_uniform_card_u32((2**32 - 6) // 10, ctypes.byref(rej))   # lo = 2^32-6 > zone
     assert rej.value == 1
+    # the stream's card rule on 16-bit halves (DESIGN §2 "cards"): every card 1..10
+    # takes exactly 6553 of the 65530 accepted halves, 6 halves are rejected
+    counts = [0] * 11
+    nrej = 0
+    for h in range(1 << 16):
+        c = L.rlo_uniform_card_u16(h, ctypes.byref(rej))
+        if rej.value:
+            nrej += 1
+        else:
+            counts[c] += 1
+    assert nrej == 6 and counts[0] == 0 and counts[1:] == [6553] * 10
+    # the stream's eps test (DESIGN §2 "draws"): the high word decides it, or asks
+    # for the low word, and always agrees with UniformFloat(h, l) < eps
+    import random
+    rnd = random.Random(7)
+    cases = []
+    for _ in range(3000):
+        h, l = rnd.getrandbits(32), rnd.getrandbits(32)
+        u = L.rlo_u64_to_uniform01((h << 32) | l)
+        for eps in (rnd.random(), u, math.nextafter(u, 2.0), math.nextafter(u, -1.0), (h + 0.5) * 2.0**-32,
+                    (h + 1) * 2.0**-32, h * 2.0**-32, 0.0, 1.0, 2.0, 1e-300, -1.0, float("nan")):
+            cases.append((h, l, eps, u))
+    undecided = 0
+    for h, l, eps, u in cases:
+        need = ctypes.c_int()
+        got = L.rlo_eps_test_words(h, l, eps, ctypes.byref(need))
+        assert bool(got) == (u < eps), (h, l, eps)
+        undecided += need.value
+        if not need.value:   # decided without the low word: any low word gives the same answer
+            assert bool(got) == (L.rlo_u64_to_uniform01((h << 32) | (l ^ 0xFFFFFFFF)) < eps)
+    assert 0 < undecided < len(cases) // 2
     # UniformFloat(0..1) endpoints
     assert L.rlo_u64_to_uniform01(0) == 0.0
     assert L.rlo_u64_to_uniform01(2**64 - 1) == 1.0 - 2.0**-52
