@@ -1502,7 +1502,9 @@ static int fq_merge_headroom(uint64_t groups) {
     return h > 0 ? h : 0;
 }
 /* traces grid: every contribution fl(lr * fl(td * E)) of a group step is below
- * 2^(max(code(td),1) - 1022 + k) with 2^k >= |lr| * Ebound * (1 + 2^-50), where
+ * 2^(max(code(td),1) - 1024 + k) with 2^k >= 4 * |lr| * Ebound * (1 + 2^-50) —
+ * below 2^51 units of its grid, two guard bits that let the device convert a
+ * contribution with the 1.5*2^52 magic add — where
  * Ebound bounds an accumulating trace (elegibility_traces_agent.rs:75-96: E += 1
  * on a visit, E *= gamma*lambda after each sweep): 1/(1-|gl|) for |gl| < 1, else
  * the geometric sum over the longest episode.  Same formula as the product's
@@ -1523,6 +1525,7 @@ int rlo_trace_grid_k(double lr, double gamma, double lambda_, uint32_t max_steps
     if (!(x < INFINITY)) return 1100;
     int ex;
     (void)frexp(x, &ex);
+    ex += 2;   /* two guard bits: |raw| < 2^51 */
     return ex < -1100 ? -1100 : (ex > 1100 ? 1100 : ex);
 }
 /* a value the fixed point holds exactly and in range */

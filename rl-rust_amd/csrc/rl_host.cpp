@@ -308,7 +308,9 @@ bool fix_exact(double v) {
     return x == std::rint(x);
 }
 // traces grid: every contribution fl(lr * fl(td * E)) of a group step is below
-// 2^(max(code(td),1) - 1022 + k) with 2^k >= |lr| * Ebound * (1 + 2^-50); Ebound
+// 2^(max(code(td),1) - 1024 + k) with 2^k >= 4 * |lr| * Ebound * (1 + 2^-50), i.e.
+// below 2^51 units of the grid 2^(max(code,1) - 1075 + k): the kernels convert it
+// with the 1.5*2^52 magic add (rl_train_impl.h contrib_tr); Ebound
 // bounds an accumulating trace (elegibility_traces_agent.rs:75-96: E += 1 on a
 // visit, E *= gamma*lambda per sweep).  Same formula as the oracle's
 // rlo_trace_grid_k (oracle/rlref.c).
@@ -328,6 +330,7 @@ int trace_grid_k(double lr, double gamma, double lambda, uint32_t max_steps, int
     if (!(x < INFINITY)) return 1100;
     int ex;
     (void)std::frexp(x, &ex);
+    ex += 2;   // two guard bits: |raw| < 2^51
     return ex < -1100 ? -1100 : (ex > 1100 ? 1100 : ex);
 }
 // merge grid headroom: n values below 2^(53-h) grid units sum below 2^63 for up

@@ -60,6 +60,9 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // max of the target row) keeps an f64 image of every entry beside its int64 word:
 // the step reads values (selection, TD target, Q(s,a)) without converting, and
 // the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_EARLY_COUNT
+#define RLAMD_EARLY_COUNT 0   // 1: count the step's train / episode-end lanes where their masks form (cfg 2: 147 static VALU against 144)
+#endif
 #ifndef RLAMD_TAIL
 #define RLAMD_TAIL 0   // 1: the throughput kernels' end-of-step bookkeeping as one predicated
                        // block (cfg 2: 0.2149-0.2157 ms against 0.2139-0.2145, A/B on one box)
@@ -954,7 +957,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // |td| and the trace bound (oracle rlref.c fq_step_combine)
     auto contrib_tr = [&](uint32_t idx, double d, int e) {
         if (__builtin_isfinite(d)) {
-            const int64_t raw = fq_raw(d, e);
+            // |raw| < 2^51 (trace_grid_k's guard bits): rint and the int64 conversion
+            // in one magic add (fq_raw's general conversion was 5 f64 operations)
+            const double y = __builtin_ldexp(d, -e) + 0x1.8p52;
+            const int64_t raw = (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
             if (raw) atomicAdd(&SUM[idx], (unsigned long long)raw);
         } else {
             atomicOr(&SFLW[idx >> 2], (nf_flag(d) << SFL_SH) << ((idx & 3u) * 8u));
@@ -1060,6 +1066,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             tgt_nf = ((((P == 2 && !L.dflag) ? f1 : f0) & row_mask) != 0ull);
         }
         const bool train_lane = doS && L.mode == RL_MODE_TRAIN;
+        if constexpr (RLAMD_EARLY_COUNT) {
+            // the step's counters from masks formed here (L.mode changes only in the
+            // bookkeeping): counted at the end, the flags crossed the step's branches
+            // and barriers and each ballot re-materialised its mask (2 VALU each)
+            c_train += (uint32_t)__popcll(__ballot(train_lane));
+            c_tep += (uint32_t)__popcll(__ballot(train_lane && term));
+            if (p.episodic) {
+                const bool ev_lane = doS && L.mode == RL_MODE_EVAL;
+                c_eval += (uint32_t)__popcll(__ballot(ev_lane));
+                c_eep += (uint32_t)__popcll(__ballot(ev_lane && term));
+            }
+        }
         if (!SPEC || !(sel_nan0 && (tgt_nf || !train_lane))) load_rows(s2, ra2, rb2);   // s2 == 0 on idle lanes
         else {
 #pragma unroll
@@ -1631,11 +1649,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         } else if (INSTR && p.rec && active) {
             write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
         }
-        c_train += (uint32_t)__popcll(__ballot(train));
-        c_tep += (uint32_t)__popcll(__ballot(tr));
-        if (p.episodic) {                  // run(): lanes only train, so no eval steps / episodes
-            c_eval += (uint32_t)__popcll(__ballot(doS && !train));
-            c_eep += (uint32_t)__popcll(__ballot(ev));
+        if constexpr (!RLAMD_EARLY_COUNT) {
+            c_train += (uint32_t)__popcll(__ballot(train));
+            c_tep += (uint32_t)__popcll(__ballot(tr));
+            if (p.episodic) {              // run(): lanes only train, so no eval steps / episodes
+                c_eval += (uint32_t)__popcll(__ballot(doS && !train));
+                c_eep += (uint32_t)__popcll(__ballot(ev));
+            }
         }
     }
 
