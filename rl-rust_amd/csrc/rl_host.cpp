@@ -471,11 +471,25 @@ int agent_select_kernel(rl_agent *a) {
     } else {
         a->kp.ucb_pack = (uint64_t)a->G * a->K < 65536ull ? 1 : 0;   // UCB + expected SARSA counters (KParams)
         const uint32_t g = std::min(a->G, a->L);
-        // lanes per wave (rl_kparams.h KParams::lpw): 64.  RLAMD_LPW=32/16 spreads a
-        // group over more waves; measured on cfg 4 (2^17 lanes, 2 waves per SIMD at
-        // 64): 32 -> 0.96x, 16 -> 0.58x (VGPRs then allow one group per CU), so
-        // it stays an experiment knob
+        // lanes per wave (rl_kparams.h KParams::lpw): 64, or 32 for the pair-pool
+        // traces kernel (small tables) when the lanes give fewer than 4 waves per
+        // SIMD at 64: the pool sweep is latency-bound and a wave sweeps its lanes'
+        // pool 64 items a round whatever its lane count, so half-full waves double
+        // the waves hiding latency for the same sweep work (cfg 4, 2^17 lanes: 2 ->
+        // 4 waves per SIMD, 0.612 -> 0.536 ms per launch, A/B on one box; 16 lanes
+        // per wave measured 0.58x: VGPRs then allow one group per CU).  RLAMD_LPW
+        // = 16 / 32 / 64 overrides (experiments)
         uint32_t lpw = 64;
+        {
+            const int ek = a->cfg.env.kind;
+            const bool pool = a->cfg.agent == RL_AGENT_TRACES && a->cfg.policy != RL_POLICY_NEURAL &&
+                              !(a->cfg.selector == RL_SEL_UCB && a->cfg.algo == RL_ALGO_EXPECTED_SARSA) &&
+                              (ek == RL_ENV_CLIFF_WALKING || ek == RL_ENV_FROZEN_LAKE ||
+                               ek == RL_ENV_FROZEN_LAKE_EDITED);
+            int ncu = 256;
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, a->device);
+            if (pool && ((uint64_t)a->L + 63u) / 64u < 16ull * (uint64_t)ncu) lpw = 32;
+        }
         if (const char *e = getenv("RLAMD_LPW")) {
             const uint32_t v = (uint32_t)atoi(e);
             if (v == 16 || v == 32 || v == 64) lpw = v;
