@@ -609,12 +609,12 @@ template <int ENV> struct EnvDev;
 // Truncation: (0, 0.0, true) for FrozenLake (:119-122), (pos, -1.0, true) for
 // FrozenLakeEdited (:227-231).
 // The outcome byte's reward bit means 1.0 (FrozenLake) or 10.0 (edited; else -1.0).
+// w: the table word trans[(pos, a)], read by the caller (possibly a step ahead)
 template <bool EDITED, int SLIP, bool AM>
-__device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, uint32_t &z, uint32_t a, Rng &r,
+__device__ __forceinline__ void fl_advance(bool doR, bool doS, uint32_t &pos, uint32_t &z, uint32_t w, Rng &r,
                                            const EnvTables &t, uint32_t &s2, double &rew, bool &term) {
     const bool trunc = doS && z >= t.max_steps;
     const bool st = doS && !trunc;
-    const uint32_t w = t.trans[tidx<AM, 4>(t, pos, a)];
     uint32_t i = 0;
     if (SLIP == 1 || (SLIP < 0 && t.slippery)) {      // the only draw whose value is used
         if (st) {

@@ -60,6 +60,10 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // max of the target row) keeps an f64 image of every entry beside its int64 word:
 // the step reads values (selection, TD target, Q(s,a)) without converting, and
 // the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_TRPF
+#define RLAMD_TRPF 0   // 1: FrozenLake reads the next step's transition word after the selection
+                       // (cfg 2: 0.2122-0.2139 ms against 0.2116-0.2125 without, A/B on one box)
+#endif
 #ifndef RLAMD_EARLY_COUNT
 #define RLAMD_EARLY_COUNT 0   // 1: count the step's train / episode-end lanes where their masks form (cfg 2: 147 static VALU against 144)
 #endif
@@ -988,6 +992,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
     unsigned long long *const RSUM = &ACC[4];
 
+    // FrozenLake family, one action per step (no reset-and-step): the step's table
+    // word trans[(s, a)] is read a step ahead (after the previous selection)
+    constexpr bool TRPF = RLAMD_TRPF && RS == 0 &&
+                          (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED);
+    uint32_t wpf = 0;
+    if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, L.s, L.a)];
     for (uint32_t k = 0; k < p.K; ++k) {
         // ---------------- one synchronous step: each live lane either RESETs
         // (env.reset() + get_action, src/agent.rs:83-84) or STEPs (env.step +
@@ -1038,7 +1048,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         }
         if constexpr (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED) {
             uint32_t pos = L.s;                    // reset or step in one predicated block
-            fl_advance<ENV == RL_ENV_FROZEN_LAKE_EDITED, SLIP, LDS_AM>(doR, doS, pos, L.z, L.a, L.rng, tabs, s2, r,
+            const uint32_t w = TRPF ? wpf : tabs.trans[tidx<LDS_AM, 4>(tabs, L.s, L.a)];
+            fl_advance<ENV == RL_ENV_FROZEN_LAKE_EDITED, SLIP, LDS_AM>(doR, doS, pos, L.z, w, L.rng, tabs, s2, r,
                                                                        term);
             L.ready = doR ? true : (term ? false : L.ready);
         } else if constexpr (ENV == RL_ENV_BLACKJACK && RLAMD_BJ_ONE_LOOP) {
@@ -1106,6 +1117,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
         }
         if (alive) a2 = sel_nan0 ? 0u : select(s2, ra2, rb2, rarg);
+        // the next step's table word (s2, a2) read now: the table is constant, and
+        // the read's latency then overlaps the update and its barriers
+        if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, s2, a2)];
         uint32_t d_own = 0xffffffffu;   // SPEC: the step-count entry this lane folds at step end
         if constexpr (SPEC) {
             // the step's increments go to the step counts / T[1], apart from what this

@@ -7,6 +7,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 R=${RPFX:-r03}
+if [ -n "$WITH_TESTS" ]; then bash scripts/gpu_tests.sh || exit $?; fi
 bench() {   # key, bench args
   timeout -k 10 300 python -u bench.py $2 > gpurun_out/bench_$1.log 2>&1 || { rc=$?; tail -5 gpurun_out/bench_$1.log; exit $rc; }
   grep '^{' gpurun_out/bench_$1.log | tail -1 > gpurun_out/bench_$1.json
