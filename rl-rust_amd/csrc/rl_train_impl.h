@@ -60,6 +60,9 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // max of the target row) keeps an f64 image of every entry beside its int64 word:
 // the step reads values (selection, TD target, Q(s,a)) without converting, and
 // the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_LATE_B3
+#define RLAMD_LATE_B3 1   // the step-separating barrier after the next step's env step
+#endif
 #ifndef RLAMD_TRPF
 #define RLAMD_TRPF 0   // 1: FrozenLake reads the next step's transition word after the selection
                        // (cfg 2: 0.2122-0.2139 ms against 0.2116-0.2125 without, A/B on one box)
@@ -998,6 +1001,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                           (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED);
     uint32_t wpf = 0;
     if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, L.s, L.a)];
+    // reset-and-step in effect (uniform over the block)
+    const bool rs_on = (!UCB && RS != 0) && (RS == 1 || p.reset_step);
     for (uint32_t k = 0; k < p.K; ++k) {
         // ---------------- one synchronous step: each live lane either RESETs
         // (env.reset() + get_action, src/agent.rs:83-84) or STEPs (env.step +
@@ -1063,6 +1068,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
+        // the previous step's settle (Q, flags, counters) before this step's reads:
+        // the env step above touches no shared table, so it overlaps the settle
+        // (reset-and-step reads Q for its reset lanes' selection: barrier at the end of the step)
+        if (RLAMD_LATE_B3 && k > 0 && !rs_on) __syncthreads();
         // UCB + expected SARSA (SPEC): the visible flags of row s2 decide most of
         // the step without Q values or counters (the regime is mostly
         // non-finite rows).  u_0 NaN sticks as the argmax (utils.rs:1-11); any
@@ -1610,7 +1619,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
             if (tid == 0) { T[0] += T[1]; T[1] = 0ull; }
         }
-        __syncthreads();   // Q_{t+1} complete before the next step's reads
+        // Q_{t+1} complete before the next step's reads (one action per step: after
+        // the next step's env step instead, below; reset-and-step reads Q first —
+        // and a barrier between its deal and its reads measured 0.98x on cfg 5)
+        if (!RLAMD_LATE_B3 || rs_on) __syncthreads();
         bool tr = false, ev = false;
         if constexpr (!INSTR && RLAMD_TAIL) {
             // one predicated block (no STEP / RESET branches): the STEP lanes'
