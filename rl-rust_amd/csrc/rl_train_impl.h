@@ -60,6 +60,9 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 // max of the target row) keeps an f64 image of every entry beside its int64 word:
 // the step reads values (selection, TD target, Q(s,a)) without converting, and
 // the settle, the only writer, converts once per changed entry.
+#ifndef RLAMD_NF_SKIP
+#define RLAMD_NF_SKIP 1   // f64 one-step: no pass-2 count for entries with non-finite contributions
+#endif
 #ifndef RLAMD_LATE_B3
 #define RLAMD_LATE_B3 1   // the step-separating barrier after the next step's env step
 #endif
@@ -931,8 +934,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // grid (or by the IEEE result of its non-finite ones), NaN canonical
     auto settle_fq = [&](uint32_t idx) {
         const uint32_t w = W[idx], n = w & 0xfffu;
-        if (n == 0u) return;                       // sweep form: untouched this step
         const uint32_t f = w >> 28;
+        if (n == 0u && f == 0u) return;            // sweep form: untouched this step
         double dl;
         if (f) {
             dl = nf_value(f);
@@ -1256,14 +1259,17 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     owner = old == 0u;
                 }
                 __syncthreads();   // every code in
-                // pass 2: the contribution on its entry's grid, and the count
-                if (train) {
+                // pass 2: the contribution on its entry's grid, and the count — only
+                // where every contribution was finite: an entry with non-finite kinds
+                // moves by their IEEE sum, which needs neither (settle_fq)
+                if (train && (RLAMD_NF_SKIP == 0 || fin)) {
                     const uint32_t w = W[idx];
                     if (fin && (w >> 28) == 0u) {
                         const int64_t raw = fq_raw(d, fq_grid(((w >> 16) & 0xfffu) - 1u));
                         if (raw) atomicAdd(&SUM[idx], (unsigned long long)raw);
+                        if (RLAMD_NF_SKIP) atomicAdd(&W[idx], 1u);
                     }
-                    atomicAdd(&W[idx], 1u);
+                    if (!RLAMD_NF_SKIP) atomicAdd(&W[idx], 1u);
                 }
                 __syncthreads();   // all contributions in, all Q reads done
                 if (sweep) { if (tid < PSAL) settle_fq(tid); }
