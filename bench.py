@@ -12,18 +12,20 @@ the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
   python bench.py [--gpus N --steps K --warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Multi-GPU: one process per GPU, lanes partitioned by global id; the merge delta
-is all-reduced by librlamd itself (rl_comm_* / rl_agent_set_comm: RCCL int64 sum
-over xGMI, the path's only collective).  torch.distributed (gloo) is the control
-plane only: it hands rank 0's RCCL id to the other ranks, runs the barriers
-around the timed region and takes the max time over ranks.
-RLAMD_COLLECTIVE=torch swaps in a torch all_reduce of the delta (a rehearsal
-mode for ranks sharing one GPU, where RCCL cannot run).
+No PyTorch: the stream, the kernel timing (HIP events, rl_agent_get_timing) and,
+for N>1, the communicator all come from librlamd.
+Multi-GPU: one process per GPU, lanes partitioned by global id; the merge buffer
+is all-reduced by librlamd itself (rl_comm_* / rl_agent_set_comm: RCCL int64
+all-reduces over xGMI, the path's only collectives).  Rank 0's RCCL id reaches the
+other ranks through a file (one node); the barriers around the timed region and
+the max time over ranks are RCCL all-reduces too (rl_comm_allreduce_f64).
+RLAMD_COLLECTIVE=torch swaps in a torch all_reduce of the merge buffer (a
+rehearsal mode for ranks sharing one GPU, where RCCL cannot run; it imports torch).
 
-Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel
-(k_train_shared) against HBM with SURVEY §8(d)'s 32 B/env-step; `cpu_baseline`
-times the oracle's faithful single-env restatement of the reference loop on
-one host core (bounded sample).
+Prints ONE JSON line on rank 0.  `roofline` names the dominant kernel's binding
+ceiling from the PMC counters of this very build (profiles/counters.json, matched
+by rl_build_id), see roofline(); `cpu_baseline` times C restatements of the
+reference loop on the host cores (bounded samples).
 """
 import argparse
 import json
@@ -57,6 +59,8 @@ def parse():
                     help="batched schedule: resetting lanes also step in the same synchronous step "
                          "(rl_agent_set_reset_step; eps-greedy)")
     ap.add_argument("--slippery", type=int, default=0)
+    ap.add_argument("--q-mode", default="auto", choices=["auto", "f64"],
+                    help="shared-Q representation: the proven fixed point where it applies, or f64 always")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--counters-file", default=os.path.join(ROOT, "profiles", "counters.json"),
@@ -87,11 +91,14 @@ PRESETS = {
 
 
 def workload_key(args):
-    return f"cfg{args.config}" + ("_slippery" if args.slippery else "")
+    return (f"cfg{args.config}" + ("_slippery" if args.slippery else "") +
+            (f"_{args.q_mode}" if args.q_mode != "auto" else "") + (f"_L{args.lanes}" if args.lanes != PRESETS[
+                args.config]["lanes"] else ""))
 
 
-def counters_for(args):
-    """PMC summary of the dominant kernel for this exact workload, or None"""
+def counters_for(args, build_id):
+    """PMC summary of the dominant kernel for this exact workload, collected from
+    this very library (rl_build_id's source hash equal), or None"""
     try:
         tab = json.load(open(args.counters_file))
     except (OSError, ValueError):
@@ -100,8 +107,11 @@ def counters_for(args):
     if not c:
         return None
     want = {"env": args.env, "algo": args.algo, "lanes": args.lanes, "group": args.group, "sync": args.sync,
-            "slippery": args.slippery, "reset_step": args.reset_step}
-    return c if all(c.get(k) == v for k, v in want.items()) else None
+            "slippery": args.slippery, "reset_step": args.reset_step, "q_mode": args.q_mode}
+    if not all(c.get(k, "auto" if k == "q_mode" else None) == v for k, v in want.items()):
+        return None
+    src = (c.get("build_id") or "").split(" ")[0]
+    return c if src and src == build_id.split(" ")[0] else None
 
 
 def cpu_baseline(args):
@@ -177,25 +187,120 @@ def cpu_baseline(args):
     return res
 
 
+def roofline(args, agent, steps_done, avg_kern_s, pmc):
+    """The dominant kernel against its binding ceiling.
+
+    Counters (profiles/counters.json) are attached only when they were collected
+    from this very library (rl_build_id equal), else `counters` is null.  With
+    them: the VALU pipe occupancy of the gfx950 model (2 cycles per wave64 VALU
+    instruction, +2 for an f64 / int64 one, +6 for an f64 transcendental;
+    MI355X_MICROARCH.md) against 1.0, and `bound` "latency" when waves wait more
+    than 40 % of their cycles while the pipe is below 70 %,
+    "valu" when the pipe is the closer ceiling, else "hbm".  The HBM side is
+    reported as measured traffic (PMC) and as the fused kernel's algorithmic bytes
+    (every lane record read and written once per launch), both <= 1 of the peak.
+    SURVEY §8(d)'s 32 B/env-step price assumes a lane-record round trip per step,
+    which the fused kernel does not make; it is kept under `hbm_priced` as a ratio,
+    not a fraction."""
+    n_act = {"frozen_lake": 4, "cliff_walking": 4, "taxi": 6, "blackjack": 2}[args.env]
+    st = agent.stats()
+    v_bar = st["trace_states"] / max(st["train_steps"], 1) if args.agent == "traces" else 0.0
+    bytes_per_step = BYTES_PER_STEP + (16 * n_act + 2) * v_bar
+    priced = bytes_per_step * steps_done / args.steps / avg_kern_s
+    # fused kernel: core + rng + aux (16 B each) + episode reward (8 B), read and
+    # written once per launch; f64 tables: the group's final Q into its slot
+    lanes = args.lanes
+    groups = (lanes + args.group - 1) // args.group
+    rows = 484 if (args.env == "blackjack" and args.selector != "ucb") else agent.S   # LDS rows per group
+    slot_bytes = 8 * agent.P * rows * agent.A * groups if agent.q_repr() == "f64" else 0
+    fused_bytes = 2 * 56 * lanes + slot_bytes
+    fused_frac = fused_bytes / avg_kern_s / HBM_PEAK
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic_frac = (traffic / avg_kern_s / HBM_PEAK) if traffic else None
+    pipe = pmc.get("valu_pipe_frac") if pmc else None
+    wait = (pmc.get("wave_cycle_split") or {}).get("SQ_WAIT_ANY") if pmc else None
+    out = {"kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
+           "hbm": {"fused_bytes_per_launch": fused_bytes, "fused_frac": fused_frac,
+                   "fused_basis": "2 x 56 B lane record per lane per launch (+ 8 B x LDS entries per group "
+                                  "for f64 tables): the fused kernel keeps lanes in registers for K steps",
+                   "traffic_bytes_per_launch": traffic, "traffic_frac": traffic_frac,
+                   "peak_GBps": HBM_PEAK / 1e9},
+           "hbm_priced": {"bytes_per_env_step": bytes_per_step, "GBps_equiv": priced / 1e9,
+                          "ratio_to_peak": priced / HBM_PEAK,
+                          "basis": "SURVEY 8(d): 32 B/env-step (+ (16A+2) V-bar for traces) x env-steps per "
+                                   "launch / kernel time; a price, not traffic (ratio may exceed 1)"},
+           **({"trace_v_bar": v_bar} if args.agent == "traces" else {}),
+           "counters": pmc.get("source") if pmc else None,
+           "counters_build": pmc.get("build_id") if pmc else None}
+    if pipe is not None:
+        if wait is not None and wait > 0.4 and pipe < 0.7:
+            bound = "latency"
+        elif traffic_frac is None or pipe >= traffic_frac:
+            bound = "valu"
+        else:
+            bound = "hbm"
+        if bound == "hbm":
+            out.update(bound="hbm", achieved=traffic / avg_kern_s / 1e9, peak=HBM_PEAK / 1e9, unit="GB/s",
+                       frac=traffic_frac, traffic=traffic)
+        else:
+            out.update(bound=bound, achieved=pipe, peak=1.0, unit="VALU pipe occupancy (gfx950 model)",
+                       frac=pipe, traffic=traffic, wait_frac=wait,
+                       basis="(2 x SQ_INSTS_VALU + 2 x (f64 add/mul/fma + int64) + 6 x f64 trans) cycles / "
+                             "(cycles x 1024 SIMDs); 'latency': SQ_WAIT_ANY > 0.4 of wave cycles with the pipe < 0.7")
+    else:
+        out.update(bound="hbm", achieved=fused_bytes / avg_kern_s / 1e9, peak=HBM_PEAK / 1e9, unit="GB/s",
+                   frac=fused_frac, traffic=None,
+                   basis="no counters from this build: the fused kernel's algorithmic bytes (hbm.fused_basis)")
+    return out
+
+
+def rccl_bootstrap(rank, world, dev):
+    """RCCL communicator without a torch control plane: rank 0's unique id is handed
+    to the other ranks through a file (one node: every rank shares /tmp), keyed by
+    the launcher's pid and MASTER_PORT so concurrent jobs never mix."""
+    import rlamd
+    path = f"/tmp/rlamd_commid_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    if rank == 0:
+        uid = rlamd.comm_unique_id()
+        with open(path + ".tmp", "wb") as f:
+            f.write(uid)
+        os.replace(path + ".tmp", path)
+    else:
+        t0 = time.time()
+        while not os.path.exists(path):
+            if time.time() - t0 > 300:
+                raise RuntimeError(f"rank {rank}: no RCCL id from rank 0 at {path}")
+            time.sleep(0.01)
+        uid = open(path, "rb").read()
+    comm = rlamd.Comm(rank, world, uid, dev)     # collective: every rank has read the id
+    comm.barrier()
+    if rank == 0:
+        os.remove(path)
+    return comm
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # RLAMD_FORCE_COMM=1 (tests): take the multi-GPU code path (gloo control plane,
-    # librlamd's RCCL communicator attached) even with one rank
+    # RLAMD_FORCE_COMM=1 (tests): take the multi-GPU code path (librlamd's RCCL
+    # communicator attached) even with one rank
     dist_on = world > 1 or os.environ.get("RLAMD_FORCE_COMM") == "1"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch  # loaded before librlamd so both share one HIP runtime
-    import torch.distributed as dist
-
-    # one process per GPU.  collective "rccl" (default): librlamd's own RCCL
-    # all-reduce, torch's gloo group only bootstraps / times.  "torch": a
-    # dist.all_reduce of the delta (rehearsal; ranks may share a device)
+    # collective "rccl" (default): librlamd's own RCCL all-reduce in every merge,
+    # and its communicator also runs the barriers and the max-over-ranks time —
+    # no PyTorch anywhere.  "torch": a torch.distributed all_reduce of the merge
+    # buffer, a rehearsal for ranks sharing one GPU, where RCCL cannot run.
     collective = os.environ.get("RLAMD_COLLECTIVE", "rccl")
-    dev = local_rank if collective == "rccl" else local_rank % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev)
-    if dist_on:
+    torch = dist = None
+    if dist_on and collective != "rccl":
+        import torch
+        import torch.distributed as dist
+        dev = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
         dist.init_process_group(os.environ.get("RLAMD_DIST_BACKEND", "gloo"))
+    else:
+        dev = local_rank
     import rlamd
 
     p = rlamd.default_params(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
@@ -206,17 +311,15 @@ def main():
     agent = rlamd.Agent(p)
     if args.reset_step:
         agent.set_reset_step(True)
+    if args.q_mode != "auto":
+        agent.set_q_mode(args.q_mode)
     occ = agent.occupancy()   # resident learner groups per CU (LDS / VGPR limited)
-    stream = torch.cuda.Stream()            # a real (non-null) HIP stream shared by torch and librlamd
-    torch.cuda.set_stream(stream)
-    agent.set_stream(stream.cuda_stream)
     delta, comm = None, None
     if dist_on and collective == "rccl":
-        box = [rlamd.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        comm = rlamd.Comm(rank, world, box[0], dev)
-        agent.set_comm(comm)                # every merge: RCCL int64 sum of the delta, then apply
+        comm = rccl_bootstrap(rank, world, dev)
+        agent.set_comm(comm)                # every merge: RCCL all-reduces over xGMI, then apply
     elif dist_on:
+        agent.set_stream(torch.cuda.current_stream().cuda_stream)
         delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
         agent.set_merge_groups(world * ((args.lanes + args.group - 1) // args.group))
@@ -232,24 +335,23 @@ def main():
         dist.all_reduce(delta[mw:])
         agent.launch_apply()
 
+    def barrier():
+        agent.synchronize()
+        if comm is not None:
+            comm.barrier()
+        elif dist is not None:
+            dist.barrier()
+        agent.synchronize()
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier()
     st0 = agent.stats()
-    agent.set_timing(True)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    agent.set_timing(True)                  # HIP events around every train kernel, on its stream
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier()
     wall = time.perf_counter() - t0
     kern_ms, n_kern = agent.timing()
     st1 = agent.stats()
@@ -257,7 +359,10 @@ def main():
     # RESET steps (env.reset + first get_action) are not env steps
     steps_done = st1["train_steps"] - st0["train_steps"]
     assert 0 < steps_done <= args.steps * args.sync * args.lanes, steps_done
-    if dist_on:                           # control plane (gloo, host tensors)
+    if comm is not None:                  # control plane over RCCL (librlamd)
+        wall = float(comm.allreduce([wall], "max")[0])
+        total_steps = int(comm.allreduce([float(steps_done)], "sum")[0])
+    elif dist is not None:                # rehearsal: gloo, host tensors
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
@@ -268,31 +373,9 @@ def main():
         total_steps = steps_done
     value = total_steps / wall
     avg_kern_s = kern_ms / max(n_kern, 1) / 1e3
-    # 32 B per env-step; traces add (16*A + 2) B per visited state
-    # swept (f64 trace read + write per action, u16 slot id), V-bar counted on the device
-    n_act = {"frozen_lake": 4, "cliff_walking": 4, "taxi": 6, "blackjack": 2}[args.env]
-    v_bar = (st1["trace_states"] - st0["trace_states"]) / max(steps_done, 1)
-    bytes_per_step = BYTES_PER_STEP + (16 * n_act + 2) * v_bar
-    bytes_per_launch = bytes_per_step * steps_done / args.steps
-    achieved = bytes_per_launch / avg_kern_s
-    pmc = counters_for(args)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    # VALU issue occupancy: ROCm's VALUBusy (SQ_ACTIVE_INST_VALU, 4 cycles per wave64
-    # VALU instruction per SIMD).  Cross-check: SQ_INSTS_VALU x 4 cycles matches the
-    # kernel's cycles on cfg 2 / 5, i.e. these kernels are VALU-issue bound
-    issue = (pmc.get("valu_busy_rocm") or pmc.get("valu_busy_frac")) if pmc else None
-    priced = achieved / HBM_PEAK
-    traffic_frac = (traffic / avg_kern_s / HBM_PEAK) if traffic else None
+    bid = rlamd.build_id()
+    pmc = counters_for(args, bid)
     q_repr = agent.q_repr()
-    # the binding limit measured by the PMC passes: VALU issue when it is closer
-    # to its ceiling than the HBM traffic is to its own
-    valu_bound = issue is not None and traffic_frac is not None and issue > traffic_frac
-    hbm_priced = {"achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": priced,
-                  "basis": "SURVEY 8(d) algorithmic bytes per env-step x env-steps per launch / kernel time"}
-    if valu_bound:
-        roof = {"bound": "valu", "achieved": issue, "peak": 1.0, "unit": "VALU-busy fraction", "frac": issue}
-    else:
-        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": priced}
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
@@ -305,28 +388,20 @@ def main():
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
                                f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
                    "survey_cfg": args.config,
-                   "schedule": "reset-and-step" if args.reset_step else "one action per synchronous step", "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
+                   "schedule": "reset-and-step" if args.reset_step else "one action per synchronous step",
+                   "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
-                   "collective": ("rccl int64 all-reduce of the merge delta (librlamd)" if collective == "rccl"
+                   "collective": ("rccl int64 all-reduces of the merge buffer (librlamd)" if collective == "rccl"
                                   else "torch all_reduce (rehearsal)") if dist_on else "none",
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"],
-                   "q_repr": q_repr},
+                   "q_repr": q_repr, "q_mode": args.q_mode},
         "build": rlamd.lib().rl_build_info().decode(),
-        # `roofline` names the measured binder (PMC passes, profiles/counters.json):
-        # `issue_frac` VALU busy, `traffic_frac` the measured HBM bytes against the
-        # peak; `hbm_priced` prices SURVEY §8(d)'s algorithmic bytes (32 B/env-step:
-        # the fused kernel keeps lane records in registers for K steps, so the
-        # measured traffic is far below them)
-        "roofline": {**roof, "traffic": traffic, "traffic_frac": traffic_frac, "issue_frac": issue,
-                     "hbm_priced": hbm_priced, "priced_frac": priced,
-                     "issue_basis": "VALU busy = SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles) (ROCm VALUBusy)",
-                     "counters": pmc.get("source") if pmc else None,
-                     "kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
-                     "kernel_launches": n_kern,
-                     "bytes_per_launch": bytes_per_launch, "bytes_per_env_step": bytes_per_step,
-                     **({"trace_v_bar": v_bar} if args.agent == "traces" else {})},
-        "torch_event_ms": ev0.elapsed_time(ev1),
+        "build_id": bid,
+        "roofline": roofline(args, agent, steps_done, avg_kern_s, pmc),
+        "timing": {"wall_s": wall, "kernel_launches_timed": n_kern,
+                   "kernel_ms_total": kern_ms, "host": "time.perf_counter between barriers; kernels: HIP "
+                                                       "events on the agent's stream (rl_agent_get_timing)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
@@ -335,7 +410,7 @@ def main():
     agent.close()
     if comm is not None:
         comm.close()
-    if dist_on:
+    if dist is not None:
         dist.destroy_process_group()
 
 

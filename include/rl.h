@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 4
+#define RL_ABI_VERSION 5
 
 enum rl_status {
     RL_OK = 0,
@@ -91,7 +91,14 @@ enum rl_lane_mode { RL_MODE_TRAIN = 0, RL_MODE_EVAL = 1, RL_MODE_DONE = 2 };
  *   RL_QREPR_PRIVATE: group_size 1, each lane an f64 reference agent.
  * A step's simultaneous contributions to one entry are combined order-free:
  * their mean, with the sum formed exactly on the integer grid of the largest
- * one (one contribution: exactly Q += lr * td, tabular_policy.rs:35-38). */
+ * one.  One contribution of a one-step agent is exactly Q += lr * td
+ * (tabular_policy.rs:35-38).  Two exceptions: eligibility traces
+ * round every lr * (td * E) of a group step onto one grid per step, 2^(code of the
+ * step's largest |td| - 1075 + trace_k), so a single-lane shared traces agent
+ * differs from the reference loop at about 1e-13 relative (private mode,
+ * group_size 1, is the reference loop bit for bit); and when the learner groups
+ * over every rank exceed 1024, the merge grid gives up ceil(log2(groups)) - 10
+ * low bits of headroom, also for entries only one group changed. */
 enum rl_q_repr { RL_QREPR_FIXED40 = 0, RL_QREPR_F64 = 1, RL_QREPR_PRIVATE = 2 };
 enum rl_q_mode {        /* rl_agent_set_q_mode */
     RL_QMODE_AUTO = 0,  /* the fixed point where proven (and the table is exact in it), else f64 */
@@ -175,11 +182,17 @@ typedef struct rl_stats {
     uint64_t eval_episodes;
     int64_t reward_sum_q16;   /* sum of training-episode rewards, fixed point 2^-16 */
     uint64_t done_lanes;      /* lanes that finished the current train()/evaluate() call */
-    uint64_t launches;
+    uint64_t launches;        /* train launches queued; each train() / evaluate() call counts
+                                 one launch past its last working one (the exit test reads
+                                 the control word one launch behind; that launch is a no-op) */
     uint64_t trace_states;    /* traces agents: sum over training steps of the visited-set size
                                  swept by the eligibility update (mean = V-bar of SURVEY 8(d)) */
     /* ABI v3 counted updates clamped to a fixed-point range; since v4 no range is
-     * ever clamped (rl_q_repr), so both stay 0 */
+     * ever clamped (rl_q_repr), so q_clamp_hits stays 0.  delta_saturations counts
+     * f64 merge entries changed by more learner groups than the merge grid's
+     * headroom allows (more than rl_agent_set_merge_groups declared, external
+     * collectives only): such a merge is not exact, and train / evaluate return
+     * RL_E_STATE when it happens */
     uint64_t q_clamp_hits;
     uint64_t delta_saturations;
 } rl_stats;
@@ -191,14 +204,22 @@ typedef struct rl_comm rl_comm;
 /* ---------------------------------------------------------------- misc */
 const char *rl_last_error(void);
 int rl_abi_version(void);
-/* how this librlamd.so was built: compiler flags, target, experiment switches */
+/* how this librlamd.so was built: compiler flags, target, experiment switches, build id */
 const char *rl_build_info(void);
+/* "src:<16 hex> git:<12 hex>": the first 16 hex digits of the sha256 of every
+ * source the library was built from (rl-rust_amd/Makefile ID_SRCS, in that order)
+ * and the git HEAD at link time.  Profiles and bench lines carry it, so numbers
+ * can be matched to the binary that produced them. */
+const char *rl_build_id(void);
 int rl_device_count(int *count);
 /* usize observation id of the reference's Blackjack env: fxhash 0.2.1 of
  * BlackJackObservation{p_score,d_score,p_ace} (src/env/blackjack.rs:25-27). */
 uint64_t rl_blackjack_obs_id(uint32_t p_score, uint32_t d_score, uint32_t p_ace);
 /* dense state index <-> reference observation (Blackjack: fxhash id; others: identity) */
 uint64_t rl_obs_to_reference(int32_t env_kind, uint32_t dense_state);
+/* the inverse: a reference observation (usize; Blackjack: its fxhash id) as the
+ * dense state index; RL_E_ARG when it is none of the env's observations */
+int rl_obs_from_reference(int32_t env_kind, uint64_t obs, uint32_t *dense_state);
 /* |S| and COUNT (Env::action_size, src/env.rs:20-22) for an env config */
 int rl_env_dims(const rl_env_config *cfg, uint32_t *n_states, uint32_t *n_actions);
 /* Host-side export of the packed device transition tables, decoded to the
@@ -220,6 +241,13 @@ int rl_env_reset(rl_env *env, uint64_t *obs_out);
 int rl_env_step(rl_env *env, const uint32_t *actions, uint64_t *obs_out, double *reward_out,
                 uint8_t *terminated_out);
 
+/* One lane's Env::reset / Env::step (the reference's single env, src/env.rs:23-24):
+ * RL_E_NOT_READY when that lane terminated and was not reset; the other lanes are
+ * untouched.  `action` as usize, obs as the reference's usize id. */
+int rl_env_reset_lane(rl_env *env, uint32_t lane, uint64_t *obs);
+int rl_env_step_lane(rl_env *env, uint32_t lane, uint32_t action, uint64_t *obs, double *reward,
+                     uint8_t *terminated);
+
 /* ---------------------------------------------------------------- Agent (batched) */
 int rl_agent_create(const rl_agent_config *cfg, rl_agent **out);
 void rl_agent_destroy(rl_agent *a);
@@ -236,6 +264,36 @@ int rl_agent_reset(rl_agent *a);
 int rl_agent_train(rl_agent *a, uint64_t n_episodes, uint64_t eval_at, rl_stats *out);
 /* Agent::evaluate(env, n_episodes) (src/agent.rs:120-141) for every lane */
 int rl_agent_evaluate(rl_agent *a, uint64_t n_episodes, rl_stats *out);
+/* ---- the per-call Agent surface: the required methods of trait Agent
+ * (src/agent.rs:52-62) on one lane's agent, so that `impl Agent<usize, COUNT> for
+ * GpuAgent` exists and the reference's default train / evaluate
+ * (src/agent.rs:66-141) and the bins' direct loops (src/bin/blackjack.rs:183-200)
+ * run over it unchanged.  Private mode (group_size 1) only: every lane is a whole
+ * reference agent (RL_E_STATE otherwise).  Observations are the reference's usize
+ * ids (Blackjack: the fxhash id, rl_obs_to_reference), as rl_env_reset / step return
+ * them.  The selector's draws come from the lane's RNG stream; an Env view of the
+ * same agent (rl_agent_env) draws the env's from that same stream, which is how
+ * the reference's one thread_rng serves both.  Each call is one kernel launch and
+ * one round trip: the compatibility path, not the throughput one (rl_agent_train). */
+/* Agent::get_action(&obs) (src/agent.rs:52; one_step_agent.rs:48-51): ε-greedy
+ * draws / UCB counter increments happen as in the reference */
+int rl_agent_get_action(rl_agent *a, uint32_t lane, uint64_t obs, uint32_t *action);
+/* Agent::update(curr_obs, curr_action, reward, terminated, next_obs, next_action)
+ * (src/agent.rs:54-62; one_step_agent.rs:53-86, elegibility_traces_agent.rs:61-104,
+ * internal_model_agent.rs:47-77 when planning is on): *td = the TD error it returns */
+int rl_agent_update(rl_agent *a, uint32_t lane, uint64_t curr_obs, uint32_t curr_action, double reward,
+                    int32_t terminated, uint64_t next_obs, uint32_t next_action, double *td);
+/* the same two for every lane at once (arrays of n_lanes; lane i is agent i) */
+int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions);
+int rl_agent_updates(rl_agent *a, const uint64_t *curr_obs, const uint32_t *curr_action, const double *reward,
+                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td);
+/* An Env over the agent's own lanes (one env per lane, the agent's RNG streams and
+ * tables, the agent's stream): rl_env_reset / rl_env_step on it are Env::reset /
+ * Env::step of the lane's env.  One view per agent; destroy it (rl_env_destroy)
+ * before the agent.  train / evaluate start every lane at a fresh reset, so the
+ * per-call and the batched loops can be mixed on one agent. */
+int rl_agent_env(rl_agent *a, rl_env **out);
+
 /* Throughput mode: enqueue n launches of K = sync_every synchronous steps over
  * all lanes (lanes train forever, episodes restart), each followed by the group
  * merge.  Asynchronous on the handle's stream. */
@@ -322,6 +380,11 @@ int rl_comm_init(int32_t rank, int32_t world, const void *id /* RL_COMM_ID_BYTES
                  rl_comm **out);
 void rl_comm_destroy(rl_comm *c);
 int rl_comm_rank(rl_comm *c, int32_t *rank, int32_t *world);
+/* host values all-reduced over the communicator's ranks, in place: op 0 = sum,
+ * 1 = max, 2 = min; n == 0 is a barrier.  Blocking.  For the caller's control
+ * plane (the bench's barriers and max-over-ranks time) — the merge's collectives
+ * run inside the launches. */
+int rl_comm_allreduce_f64(rl_comm *c, double *vals, uint32_t n, int32_t op);
 /* attach (NULL: detach) a communicator: from then on every merge of rl_agent_run /
  * rl_agent_train / rl_agent_evaluate all-reduces the delta over it (train/evaluate
  * also agree on termination across ranks).  Shared mode only. */
@@ -331,13 +394,20 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c);
 int rl_agent_sync(rl_agent *a);
 
 /* -------- multi-GPU: the merge as an external collective (shared mode) */
-/* int64 words of the merge buffer (all of it) and of its leading MAX part */
+/* int64 words of the merge buffer the current Q representation uses (all of it)
+ * and of its leading MAX part: f64 MAX [E] + SUM [E sums][E counts][S*A dN][1 dt]
+ * [3 x E non-finite kind counts], E = the learner group's LDS entries (Blackjack
+ * eps-greedy: its 2 x 484 x 2 non-terminal entries, not the 8192 dense ones); the
+ * fixed point has no MAX words and SUM [PSA dQ][PSA counts][S*A dN][1 dt].  The
+ * sizes change with the representation (rl_agent_q_repr): a caller-owned buffer
+ * must hold the current one (a launch fails with RL_E_STATE otherwise). */
 int rl_agent_delta_words(rl_agent *a, uint64_t *n);
 int rl_agent_delta_max_words(rl_agent *a, uint64_t *n);
 /* use caller-owned device memory (e.g. a torch int64 tensor, zeroed) as the buffer */
 int rl_agent_set_delta_buffer(rl_agent *a, void *device_ptr, uint64_t n_words);
 /* learner groups over every rank (the f64 merge grid's headroom; the attached
- * communicator sets it, external collectives call this); 0 = this rank's */
+ * communicator sets it, external collectives must call this before
+ * rl_agent_launch_fold: RL_E_STATE otherwise); 0 = this rank's */
 int rl_agent_set_merge_groups(rl_agent *a, uint64_t total_groups);
 /* one launch = train kernel (this device's part of the buffer) ...
  * [caller all-reduces the MAX words with MAX] ... */

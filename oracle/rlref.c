@@ -1321,13 +1321,14 @@ void rlo_faithful_set_weights(rlo_faithful *f, const double *in) {
 uint64_t rlo_faithful_n_episodes(const rlo_faithful *f) { return f->reward_history.n; }
 uint64_t rlo_faithful_n_steps(const rlo_faithful *f) { return f->training_error.n; }
 void rlo_faithful_histories(const rlo_faithful *f, double *rh, uint64_t *el, double *te) {
-    if (rh) memcpy(rh, f->reward_history.p, f->reward_history.n * sizeof(double));
-    if (el) memcpy(el, f->episode_length.p, f->episode_length.n * sizeof(uint64_t));
-    if (te) memcpy(te, f->training_error.p, f->training_error.n * sizeof(double));
+    /* memcpy with a null pointer is undefined even for 0 bytes (UBSan) */
+    if (rh && f->reward_history.n) memcpy(rh, f->reward_history.p, f->reward_history.n * sizeof(double));
+    if (el && f->episode_length.n) memcpy(el, f->episode_length.p, f->episode_length.n * sizeof(uint64_t));
+    if (te && f->training_error.n) memcpy(te, f->training_error.p, f->training_error.n * sizeof(double));
 }
 uint64_t rlo_faithful_get_records(const rlo_faithful *f, rlo_record *out, uint64_t cap) {
     uint64_t n = f->records.n < cap ? f->records.n : cap;
-    memcpy(out, f->records.p, n * sizeof(rlo_record));
+    if (n) memcpy(out, f->records.p, n * sizeof(rlo_record));
     return f->records.n;
 }
 uint64_t rlo_faithful_bench(const rlo_config *c, uint64_t n_episodes, uint64_t eval_at, double *sec) {
@@ -1515,10 +1516,11 @@ int rlo_trace_grid_k(double lr, double gamma, double lambda_, uint32_t max_steps
     if (a < 1.0) {
         eb = 1.0 / (1.0 - a);
     } else {
-        const uint32_t T = env == RLO_ENV_BLACKJACK ? 32u : max_steps + 1u;
-        double p = 1.0;
-        eb = 0.0;
-        for (uint32_t k = 0; k <= T && eb < INFINITY; ++k) { eb += p; p *= a; }
+        /* sum_{k=0..T} a^k in closed form (T in 64 bits: max_steps + 1 cannot wrap;
+         * O(1)); expm1/log1p keep it accurate for a just above 1,
+         * and it is +inf when the sum overflows */
+        const uint64_t T = env == RLO_ENV_BLACKJACK ? 32u : (uint64_t)max_steps + 1u;
+        eb = a == 1.0 ? (double)(T + 1u) : expm1((double)(T + 1u) * log1p(a - 1.0)) / (a - 1.0);
     }
     const double x = fabs(lr) * eb * (1.0 + 0x1p-50) * 1.0001;
     if (!(x > 0.0)) return 0;
@@ -2313,7 +2315,7 @@ void rlo_batch_set_ucb(rlo_batch *b, const uint64_t *counts, const uint64_t *t) 
 }
 uint64_t rlo_batch_take_records(rlo_batch *b, rlo_record *out, uint64_t cap) {
     uint64_t n = b->records.n;
-    if (out) memcpy(out, b->records.p, (n < cap ? n : cap) * sizeof(rlo_record));
+    if (out && n && cap) memcpy(out, b->records.p, (n < cap ? n : cap) * sizeof(rlo_record));
     b->records.n = 0;
     return n;
 }

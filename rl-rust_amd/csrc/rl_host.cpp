@@ -320,10 +320,11 @@ int trace_grid_k(double lr, double gamma, double lambda, uint32_t max_steps, int
     if (a < 1.0) {
         eb = 1.0 / (1.0 - a);
     } else {
-        const uint32_t T = env == RL_ENV_BLACKJACK ? 32u : max_steps + 1u;
-        double pw = 1.0;
-        eb = 0.0;
-        for (uint32_t k = 0; k <= T && eb < INFINITY; ++k) { eb += pw; pw *= a; }
+        // sum_{k=0..T} a^k in closed form (T in 64 bits: max_steps + 1 cannot wrap;
+        // O(1)); expm1/log1p keep it accurate for a just above 1, and
+        // it is +inf when the sum overflows
+        const uint64_t T = env == RL_ENV_BLACKJACK ? 32u : (uint64_t)max_steps + 1u;
+        eb = a == 1.0 ? (double)(T + 1u) : std::expm1((double)(T + 1u) * std::log1p(a - 1.0)) / (a - 1.0);
     }
     const double x = std::fabs(lr) * eb * (1.0 + 0x1p-50) * 1.0001;
     if (!(x > 0.0)) return 0;
@@ -369,12 +370,20 @@ struct rl_comm {
     ncclComm_t comm = nullptr;
     int32_t rank = 0, world = 1, device = 0;
     int64_t *word = nullptr;   // one device int64 for the done-lane agreement of train()/evaluate()
+    // host-value all-reduces (rl_comm_allreduce_f64: the bench's barrier and max time)
+    hipStream_t stream = nullptr;
+    double *vals = nullptr;
+    uint32_t n_vals = 0;
 };
 struct rl_env {
     rl_env_config cfg{};
     EnvHost eh;
     int device = 0;
     hipStream_t stream = nullptr;
+    // an Env view of an agent's lanes (rl_agent_env): lane records, RNG streams and
+    // tables are the agent's, calls run on the agent's stream
+    bool view = false;
+    rl_agent *owner = nullptr;
     uint32_t L = 0;
     uint4 *core = nullptr, *rng = nullptr;
     uint32_t *trans = nullptr;
@@ -401,9 +410,12 @@ struct rl_agent {
     int64_t *q_base = nullptr;   // fixed-point words or f64 bits (qrepr)
     uint64_t *n_base = nullptr;
     uint64_t *t_base = nullptr;
-    // merge buffer [PSA MAX words][delta_words SUM words]: own, or the caller's
+    // merge buffer [MAX words][SUM words] (merge_layout), own or the caller's:
+    // delta_cap words at delta_max, delta = delta_max + the MAX words
     int64_t *delta_own = nullptr, *delta_max = nullptr, *delta = nullptr, *delta_rep = nullptr;
-    uint64_t delta_words = 0;    // the SUM part
+    uint64_t delta_words = 0;    // replica stride: the dense SUM layout
+    uint64_t delta_cap = 0;
+    bool merge_groups_set = false;   // rl_agent_set_merge_groups / set_comm declared the total
     uint32_t n_rep = 1;
     uint64_t *qslot = nullptr;   // f64 merge: every group's final Q [n_groups][psal]
     uint32_t n_groups = 0, psal = 0;
@@ -447,6 +459,10 @@ struct rl_agent {
     int64_t *ctl_d = nullptr, *ctl_h = nullptr;
     hipEvent_t ctl_ev[2] = {nullptr, nullptr};
     KParams kp{};
+    // per-call Agent surface (rl_agent_get_action / rl_agent_update): device
+    // arrays of L entries and their pinned host staging
+    unsigned char *call_d = nullptr, *call_h = nullptr;
+    rl_env *env_view = nullptr;
     train_launch_fn fn = nullptr;
     dim3 grid, block;
     size_t smem = 0;
@@ -735,6 +751,20 @@ int agent_recheck_repr(rl_agent *a) {
     return agent_select_kernel(a);
 }
 
+// LDS-held entries per learner group: Blackjack eps-greedy keeps the 484 non-terminal rows
+uint32_t lds_entries(const rl_agent *a) {
+    return (a->cfg.env.kind == RL_ENV_BLACKJACK && a->cfg.selector != RL_SEL_UCB) ? a->P * 484u * a->A
+                                                                                 : a->P * a->S * a->A;
+}
+// words of the merge buffer the current representation uses (all-reduced):
+// f64 MAX [psal] + SUM [psal sums][psal counts][SA dN][1 dt][3 x psal kinds];
+// fixed point no MAX words, SUM [PSA dQ][PSA counts][SA dN][1 dt]
+void merge_layout(const rl_agent *a, uint64_t *max_words, uint64_t *sum_words) {
+    const uint64_t SA = (uint64_t)a->S * a->A, PSA = a->P * SA, ps = lds_entries(a);
+    if (a->qrepr == RL_QREPR_F64) { *max_words = ps; *sum_words = 5 * ps + SA + 1; }
+    else { *max_words = 0; *sum_words = 2 * PSA + SA + 1; }
+}
+
 void agent_sync_params(rl_agent *a) {
     KParams &p = a->kp;
     p.lr = a->cfg.lr;
@@ -752,13 +782,17 @@ void agent_sync_params(rl_agent *a) {
     p.pack_ok = !p.fq && pack_proven(a) ? 1 : 0;
     p.trace_k = trace_grid_k(a->cfg.lr, a->cfg.gamma, a->cfg.lambda, a->cfg.env.max_steps, a->cfg.env.kind);
     p.merge_hb = merge_headroom(a->merge_groups);
+    if (!a->priv) {
+        uint64_t mw, sw;
+        merge_layout(a, &mw, &sw);
+        a->delta = a->delta_max + mw;
+        p.sum_words = (uint32_t)sw;
+    }
     p.delta = a->delta;
     p.delta_max = a->delta_max;
     p.qslot = a->qslot;
     p.n_groups = a->n_groups;
-    // LDS-held entries per group: Blackjack eps-greedy keeps the 484 non-terminal rows
-    p.psal = (a->cfg.env.kind == RL_ENV_BLACKJACK && a->cfg.selector != RL_SEL_UCB)
-                 ? a->P * 484u * a->A : a->P * a->S * a->A;
+    p.psal = lds_entries(a);
     p.plan_steps = a->plan;
     p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;
     p.elog = a->elog_cap ? a->elog_d : nullptr;
@@ -770,6 +804,13 @@ void agent_sync_params(rl_agent *a) {
 // process, its own delta); *merge = true when the fused fold + apply did it
 int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
     agent_sync_params(a);
+    if (!a->priv) {
+        uint64_t mw, sw;
+        merge_layout(a, &mw, &sw);
+        if (mw + sw > a->delta_cap)
+            return fail(RL_E_STATE, "merge buffer smaller than the current Q representation needs "
+                                    "(rl_agent_delta_words): set a larger one");
+    }
     a->kp.episodic = (a->kp.target_episodes || a->kp.eval_at || a->kp.eval_only) ? 1 : 0;
     if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -838,14 +879,17 @@ int comm_live(rl_agent *a);
 int allreduce_max(rl_agent *a) {
     if (!a->comm || a->qrepr != RL_QREPR_F64) return RL_OK;
     if (int rc = comm_live(a)) return rc;
-    NCCLC(ncclAllReduce(a->delta_max, a->delta_max, (size_t)a->P * a->S * a->A, ncclInt64, ncclMax, a->comm->comm,
-                        a->stream));
+    uint64_t mw, sw;
+    merge_layout(a, &mw, &sw);
+    NCCLC(ncclAllReduce(a->delta_max, a->delta_max, mw, ncclInt64, ncclMax, a->comm->comm, a->stream));
     return RL_OK;
 }
 int allreduce_delta(rl_agent *a) {
     if (!a->comm) return RL_OK;   // no communicator: this process's delta is the total
     if (int rc = comm_live(a)) return rc;
-    NCCLC(ncclAllReduce(a->delta, a->delta, a->delta_words, ncclInt64, ncclSum, a->comm->comm, a->stream));
+    uint64_t mw, sw;
+    merge_layout(a, &mw, &sw);
+    NCCLC(ncclAllReduce(a->delta, a->delta, sw, ncclInt64, ncclSum, a->comm->comm, a->stream));
     return RL_OK;
 }
 // the merge after a launch: [MAX] -> fold -> [SUM] -> apply
@@ -910,6 +954,8 @@ int run_until_done(rl_agent *a, rl_stats *out) {
     const uint64_t lag = (a->recording || dump) ? 0 : 1;
     int rc = comm_live(a);
     if (rc) return rc;
+    rl_stats st0{};
+    if ((rc = rl_agent_stats(a, &st0))) return rc;
     for (uint64_t launch = 0;; ++launch) {
         int64_t status = CTL_OK;
         if (launch + 1 >= max_launches) status = CTL_LAUNCH_CAP;
@@ -946,7 +992,12 @@ int run_until_done(rl_agent *a, rl_stats *out) {
         if (w[0] >= w[1]) break;
     }
     HIPC(hipStreamSynchronize(a->stream));
-    if (out) return rl_agent_stats(a, out);
+    rl_stats st1{};
+    if ((rc = rl_agent_stats(a, &st1))) return rc;
+    if (st1.delta_saturations != st0.delta_saturations)
+        return fail(RL_E_STATE, "f64 merge over more learner groups than its headroom allows "
+                                "(rl_agent_set_merge_groups): Q is not the exact mean");
+    if (out) *out = st1;
     return RL_OK;
 }
 
@@ -963,8 +1014,10 @@ int rl_abi_version(void) { return RL_ABI_VERSION; }
 #define RLAMD_STR2(x) #x
 #define RLAMD_STR(x) RLAMD_STR2(x)
 const char *rl_build_info(void) {
-    return "librlamd abi " RLAMD_STR(RL_ABI_VERSION) "; target gfx950; RLAMD_EXP=" RLAMD_STR(RLAMD_EXP)
-           "; flags: " RLAMD_BUILD_FLAGS;
+    static const std::string s = std::string("librlamd abi " RLAMD_STR(RL_ABI_VERSION) "; target gfx950; RLAMD_EXP="
+                                             RLAMD_STR(RLAMD_EXP) "; flags: " RLAMD_BUILD_FLAGS "; id: ") +
+                                 rl_build_id();
+    return s.c_str();
 }
 int rl_device_count(int *count) {
     HIPC(hipGetDeviceCount(count));
@@ -982,6 +1035,25 @@ uint64_t rl_blackjack_obs_id(uint32_t p, uint32_t d, uint32_t ace) {
 uint64_t rl_obs_to_reference(int32_t env_kind, uint32_t s) {
     if (env_kind == RL_ENV_BLACKJACK) return rl_blackjack_obs_id(s >> 6, (s >> 1) & 31u, s & 1u);
     return s;
+}
+int rl_obs_from_reference(int32_t env_kind, uint64_t obs, uint32_t *dense_state) {
+    if (!dense_state) return fail(RL_E_ARG, "null argument");
+    if (env_kind != RL_ENV_BLACKJACK) {
+        if (obs > 0xffffffffull) return fail(RL_E_ARG, "observation out of range");
+        *dense_state = (uint32_t)obs;
+        return RL_OK;
+    }
+    // the 2048 dense Blackjack observations by their fxhash ids (distinct: checked once)
+    static const std::vector<std::pair<uint64_t, uint32_t>> ids = [] {
+        std::vector<std::pair<uint64_t, uint32_t>> v(2048);
+        for (uint32_t s = 0; s < 2048; ++s) v[s] = {rl_obs_to_reference(RL_ENV_BLACKJACK, s), s};
+        std::sort(v.begin(), v.end());
+        return v;
+    }();
+    const auto it = std::lower_bound(ids.begin(), ids.end(), std::make_pair(obs, 0u));
+    if (it == ids.end() || it->first != obs) return fail(RL_E_ARG, "not a Blackjack observation id");
+    *dense_state = it->second;
+    return RL_OK;
 }
 
 int rl_env_dims(const rl_env_config *cfg, uint32_t *S, uint32_t *A) {
@@ -1094,19 +1166,37 @@ int rl_env_create(const rl_env_config *cfg, uint32_t n, uint64_t seed, uint64_t 
 void rl_env_destroy(rl_env *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
-    dfree(e->core); dfree(e->rng); dfree(e->act_d); dfree(e->obs_d); dfree(e->rew_d); dfree(e->term_d);
-    dfree(e->trans); dfree(e->cdf);
+    if (e->view) {   // the agent owns the lanes and tables
+        if (e->owner) {
+            (void)hipStreamSynchronize(e->owner->stream);
+            e->owner->env_view = nullptr;
+        }
+    } else {
+        dfree(e->core); dfree(e->rng); dfree(e->trans); dfree(e->cdf);
+    }
+    dfree(e->act_d); dfree(e->obs_d); dfree(e->rew_d); dfree(e->term_d);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
+namespace {
+// the stream an Env call runs on: its own, or its agent's for a view
+int env_stream(rl_env *e, hipStream_t *st) {
+    if (e->view && !e->owner) return fail(RL_E_STATE, "Env view used after its agent was destroyed");
+    *st = e->view ? e->owner->stream : e->stream;
+    HIPC(hipSetDevice(e->device));
+    return RL_OK;
+}
+}  // namespace
+
 int rl_env_reset(rl_env *e, uint64_t *obs) {
     if (!e || !obs) return fail(RL_E_ARG, "null argument");
-    HIPC(hipSetDevice(e->device));
-    launch_env_reset(e->cfg.kind, e->kp, e->stream, e->obs_d);
+    hipStream_t st;
+    if (int rc = env_stream(e, &st)) return rc;
+    launch_env_reset(e->cfg.kind, e->kp, st, e->obs_d);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPC(hipStreamSynchronize(e->stream));
+    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < e->L; ++i) obs[i] = rl_obs_to_reference(e->cfg.kind, (uint32_t)obs[i]);
     std::fill(e->ready.begin(), e->ready.end(), 1);
     return RL_OK;
@@ -1118,18 +1208,58 @@ int rl_env_step(rl_env *e, const uint32_t *act, uint64_t *obs, double *rew, uint
         if (!e->ready[i]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(i));
         if (act[i] >= e->eh.A) return fail(RL_E_ARG, "action out of range");
     }
-    HIPC(hipSetDevice(e->device));
-    HIPC(hipMemcpyAsync(e->act_d, act, e->L * 4, hipMemcpyHostToDevice, e->stream));
-    launch_env_step(e->cfg.kind, e->kp, e->stream, e->act_d, e->obs_d, e->rew_d, e->term_d, nullptr);
+    hipStream_t st;
+    if (int rc = env_stream(e, &st)) return rc;
+    HIPC(hipMemcpyAsync(e->act_d, act, e->L * 4, hipMemcpyHostToDevice, st));
+    launch_env_step(e->cfg.kind, e->kp, st, e->act_d, e->obs_d, e->rew_d, e->term_d, nullptr);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPC(hipMemcpyAsync(rew, e->rew_d, e->L * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPC(hipMemcpyAsync(term, e->term_d, e->L, hipMemcpyDeviceToHost, e->stream));
-    HIPC(hipStreamSynchronize(e->stream));
+    HIPC(hipMemcpyAsync(obs, e->obs_d, e->L * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(rew, e->rew_d, e->L * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(term, e->term_d, e->L, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < e->L; ++i) {
         obs[i] = rl_obs_to_reference(e->cfg.kind, (uint32_t)obs[i]);
         if (term[i]) e->ready[i] = 0;
     }
+    return RL_OK;
+}
+
+// one lane's Env::reset / Env::step (the reference's single env): the batched
+// kernels over a one-lane window of the records
+int rl_env_reset_lane(rl_env *e, uint32_t lane, uint64_t *obs) {
+    if (!e || !obs) return fail(RL_E_ARG, "null argument");
+    if (lane >= e->L) return fail(RL_E_ARG, "lane out of range");
+    hipStream_t st;
+    if (int rc = env_stream(e, &st)) return rc;
+    KParams p = e->kp;
+    p.L = 1; p.core += lane; p.rng += lane;
+    launch_env_reset(e->cfg.kind, p, st, e->obs_d);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(obs, e->obs_d, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    *obs = rl_obs_to_reference(e->cfg.kind, (uint32_t)*obs);
+    e->ready[lane] = 1;
+    return RL_OK;
+}
+
+int rl_env_step_lane(rl_env *e, uint32_t lane, uint32_t action, uint64_t *obs, double *rew, uint8_t *term) {
+    if (!e || !obs || !rew || !term) return fail(RL_E_ARG, "null argument");
+    if (lane >= e->L) return fail(RL_E_ARG, "lane out of range");
+    if (!e->ready[lane]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(lane));
+    if (action >= e->eh.A) return fail(RL_E_ARG, "action out of range");
+    hipStream_t st;
+    if (int rc = env_stream(e, &st)) return rc;
+    KParams p = e->kp;
+    p.L = 1; p.core += lane; p.rng += lane;
+    HIPC(hipMemcpyAsync(e->act_d, &action, 4, hipMemcpyHostToDevice, st));
+    launch_env_step(e->cfg.kind, p, st, e->act_d, e->obs_d, e->rew_d, e->term_d, nullptr);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(obs, e->obs_d, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(rew, e->rew_d, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(term, e->term_d, 1, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    *obs = rl_obs_to_reference(e->cfg.kind, (uint32_t)*obs);
+    if (*term) e->ready[lane] = 0;
     return RL_OK;
 }
 
@@ -1192,6 +1322,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
             return bad(rc);
         a->delta_max = a->delta_own;
         a->delta = a->delta_own + PSA;
+        a->delta_cap = PSA + a->delta_words;   // the largest layout: f64 over dense rows
         if (hipMemset(a->delta_own, 0, (PSA + a->delta_words) * 8) != hipSuccess) return bad(fail(RL_E_HIP, "memset"));
         a->n_rep = std::min<uint32_t>(64u, n_groups);
         if ((rc = dalloc(&a->delta_rep, a->delta_words * a->n_rep))) return bad(rc);
@@ -1238,6 +1369,7 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.delta_rep = a->delta_rep;
     p.n_rep = a->n_rep;
     p.delta_words = (uint32_t)a->delta_words;
+    p.sum_words = (uint32_t)a->delta_words;
     p.q_priv = a->q_priv; p.n_priv = a->n_priv; p.t_priv = a->t_priv;
     p.net_w = a->net_w; p.feat = a->feat; p.n_in = a->n_in; p.n_hidden = c.net.hidden; p.n_params = a->n_params;
     p.act1 = c.net.act_hidden; p.act2 = c.net.act_out;
@@ -1272,7 +1404,9 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
-    dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d);
+    dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d); dfree(a->call_d);
+    if (a->call_h) (void)hipHostFree(a->call_h);
+    if (a->env_view) a->env_view->owner = nullptr;   // the view outlives its agent: calls fail with RL_E_STATE
     if (a->ctl_h) (void)hipHostFree(a->ctl_h);
     for (hipEvent_t e : a->ctl_ev)
         if (e) (void)hipEventDestroy(e);
@@ -1570,6 +1704,135 @@ int rl_agent_get_epsilon(rl_agent *a, double *out, size_t n) {
     return RL_OK;
 }
 
+// ---------------------------------------------------------------- per-call Agent surface
+namespace {
+// call buffer of L entries: [r f64][td f64][s][a][s2][a2][action u32][term u8]
+struct CallLayout {
+    size_t r, td, s, a, s2, a2, act, term, total;
+    explicit CallLayout(size_t L) {
+        r = 0; td = 8 * L; s = 16 * L; a = s + 4 * L; s2 = a + 4 * L; a2 = s2 + 4 * L; act = a2 + 4 * L;
+        term = act + 4 * L; total = term + L;
+    }
+};
+// the reference observation (usize) of a lane as a dense state index
+int dense_of(const rl_agent *a, uint64_t obs, uint32_t *out) {
+    uint32_t d = 0;
+    if (rl_obs_from_reference(a->cfg.env.kind, obs, &d) != RL_OK || d >= a->S)
+        return fail(RL_E_ARG, "observation " + std::to_string(obs) + " is not a state of this env");
+    *out = d;
+    return RL_OK;
+}
+// get_action (op CALL_GET_ACTION) or update (CALL_UPDATE) on lanes [lane0, lane0 + n)
+int agent_call(rl_agent *a, int op, uint32_t lane0, uint32_t n, const uint64_t *s, const uint32_t *act,
+               const double *r, const uint8_t *term, const uint64_t *s2, const uint32_t *a2, uint32_t *action_out,
+               double *td_out) {
+    if (!a->priv) return fail(RL_E_STATE, "get_action / update are per-agent calls: private mode (group_size 1) only");
+    if (n == 0) return RL_OK;
+    if ((uint64_t)lane0 + n > a->L) return fail(RL_E_ARG, "lane out of range");
+    HIPC(hipSetDevice(a->device));
+    const CallLayout cl(a->L);
+    if (!a->call_d) {
+        if (int rc = dalloc(&a->call_d, cl.total)) return rc;
+        HIPC(hipHostMalloc((void **)&a->call_h, cl.total, hipHostMallocDefault));
+    }
+    unsigned char *h = a->call_h;
+    uint32_t *hs = (uint32_t *)(h + cl.s), *ha = (uint32_t *)(h + cl.a), *hs2 = (uint32_t *)(h + cl.s2),
+             *ha2 = (uint32_t *)(h + cl.a2);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (int rc = dense_of(a, s[i], &hs[i])) return rc;
+        if (op == CALL_UPDATE) {
+            if (int rc = dense_of(a, s2[i], &hs2[i])) return rc;
+            if (act[i] >= a->A || a2[i] >= a->A) return fail(RL_E_ARG, "action out of range");
+            ha[i] = act[i];
+            ha2[i] = a2[i];
+            ((double *)(h + cl.r))[i] = r[i];
+            h[cl.term + i] = term[i] ? 1 : 0;
+        }
+    }
+    // inputs: one copy of the used span (s .. term) plus r
+    HIPC(hipMemcpyAsync(a->call_d + cl.s, h + cl.s, cl.total - cl.s, hipMemcpyHostToDevice, a->stream));
+    if (op == CALL_UPDATE) HIPC(hipMemcpyAsync(a->call_d, h, 8 * (size_t)n, hipMemcpyHostToDevice, a->stream));
+    agent_sync_params(a);
+    KParams p = a->kp;
+    p.call_op = op;
+    p.call_lane0 = lane0;
+    p.call_n = n;
+    p.call.s = (const uint32_t *)(a->call_d + cl.s);
+    p.call.a = (const uint32_t *)(a->call_d + cl.a);
+    p.call.s2 = (const uint32_t *)(a->call_d + cl.s2);
+    p.call.a2 = (const uint32_t *)(a->call_d + cl.a2);
+    p.call.r = (const double *)(a->call_d + cl.r);
+    p.call.term = a->call_d + cl.term;
+    p.call.action_out = (uint32_t *)(a->call_d + cl.act);
+    p.call.td_out = (double *)(a->call_d + cl.td);
+    const hipError_t le = a->fn(p, dim3(1), dim3(1), 0, a->stream, nullptr);
+    if (le != hipSuccess) return fail(RL_E_HIP, std::string("agent call launch: ") + hipGetErrorString(le));
+    if (op == CALL_GET_ACTION)
+        HIPC(hipMemcpyAsync(action_out, a->call_d + cl.act, 4 * (size_t)n, hipMemcpyDeviceToHost, a->stream));
+    else
+        HIPC(hipMemcpyAsync(td_out, a->call_d + cl.td, 8 * (size_t)n, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+}  // namespace
+
+int rl_agent_get_action(rl_agent *a, uint32_t lane, uint64_t obs, uint32_t *action) {
+    if (!a || !action) return fail(RL_E_ARG, "null argument");
+    return agent_call(a, CALL_GET_ACTION, lane, 1, &obs, nullptr, nullptr, nullptr, nullptr, nullptr, action,
+                      nullptr);
+}
+int rl_agent_update(rl_agent *a, uint32_t lane, uint64_t curr_obs, uint32_t curr_action, double reward,
+                    int32_t terminated, uint64_t next_obs, uint32_t next_action, double *td) {
+    if (!a || !td) return fail(RL_E_ARG, "null argument");
+    const uint8_t t = terminated ? 1 : 0;
+    return agent_call(a, CALL_UPDATE, lane, 1, &curr_obs, &curr_action, &reward, &t, &next_obs, &next_action,
+                      nullptr, td);
+}
+int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions) {
+    if (!a || !obs || !actions) return fail(RL_E_ARG, "null argument");
+    return agent_call(a, CALL_GET_ACTION, 0, a->L, obs, nullptr, nullptr, nullptr, nullptr, nullptr, actions, nullptr);
+}
+int rl_agent_updates(rl_agent *a, const uint64_t *curr_obs, const uint32_t *curr_action, const double *reward,
+                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td) {
+    if (!a || !curr_obs || !curr_action || !reward || !terminated || !next_obs || !next_action || !td)
+        return fail(RL_E_ARG, "null argument");
+    return agent_call(a, CALL_UPDATE, 0, a->L, curr_obs, curr_action, reward, terminated, next_obs, next_action,
+                      nullptr, td);
+}
+
+int rl_agent_env(rl_agent *a, rl_env **out) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    *out = nullptr;
+    if (a->env_view) return fail(RL_E_STATE, "this agent already has an Env view (rl_env_destroy it first)");
+    HIPC(hipSetDevice(a->device));
+    rl_env *e = new rl_env();
+    e->cfg = a->cfg.env;
+    e->eh = a->eh;
+    e->device = a->device;
+    e->view = true;
+    e->owner = a;
+    e->L = a->L;
+    int rc;
+    if ((rc = dalloc(&e->act_d, e->L)) || (rc = dalloc(&e->obs_d, e->L)) || (rc = dalloc(&e->rew_d, e->L)) ||
+        (rc = dalloc(&e->term_d, e->L))) {
+        rl_env_destroy(e);
+        return rc;
+    }
+    e->core = a->core; e->rng = a->rng; e->trans = a->trans; e->cdf = a->cdf;
+    KParams &p = e->kp;
+    p.L = e->L; p.S = a->S; p.A = a->A; p.P = 1;
+    p.core = a->core; p.rng = a->rng;
+    p.trans = a->trans; p.start_cdf = a->cdf; p.n_start = (uint32_t)a->eh.cdf.size();
+    p.fixed_start = a->eh.fixed_start;
+    p.slippery = a->eh.slippery;
+    p.max_steps = a->eh.max_steps; p.th1 = a->eh.th1; p.th2 = a->eh.th2; p.th3 = a->eh.th3;
+    p.trunc_reward = a->eh.trunc_reward;
+    e->ready.assign(e->L, 0);
+    a->env_view = e;
+    *out = e;
+    return RL_OK;
+}
+
 int rl_agent_set_recording(rl_agent *a, int32_t enable) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
@@ -1670,23 +1933,27 @@ int rl_agent_take_episodes(rl_agent *a, rl_episode_record *out, uint64_t cap, ui
 
 int rl_agent_delta_words(rl_agent *a, uint64_t *n) {
     if (!a || !n) return fail(RL_E_ARG, "null argument");
-    *n = a->priv ? 0 : (uint64_t)a->P * a->S * a->A + a->delta_words;
+    uint64_t mw = 0, sw = 0;
+    if (!a->priv) merge_layout(a, &mw, &sw);
+    *n = mw + sw;
     return RL_OK;
 }
 int rl_agent_delta_max_words(rl_agent *a, uint64_t *n) {
     if (!a || !n) return fail(RL_E_ARG, "null argument");
-    *n = a->priv ? 0 : (uint64_t)a->P * a->S * a->A;
+    uint64_t mw = 0, sw = 0;
+    if (!a->priv) merge_layout(a, &mw, &sw);
+    *n = mw;
     return RL_OK;
 }
 
 int rl_agent_set_delta_buffer(rl_agent *a, void *ptr, uint64_t n_words) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (a->priv) return fail(RL_E_STATE, "private mode has no merge");
-    const uint64_t PSA = (uint64_t)a->P * a->S * a->A;
-    int64_t *base = ptr ? (int64_t *)ptr : a->delta_own;
-    if (ptr && n_words < PSA + a->delta_words) return fail(RL_E_ARG, "delta buffer too small");
-    a->delta_max = base;
-    a->delta = base + PSA;
+    uint64_t mw, sw;
+    merge_layout(a, &mw, &sw);
+    if (ptr && n_words < mw + sw) return fail(RL_E_ARG, "delta buffer too small (rl_agent_delta_words)");
+    a->delta_max = ptr ? (int64_t *)ptr : a->delta_own;
+    a->delta_cap = ptr ? n_words : (uint64_t)a->P * a->S * a->A + a->delta_words;
     agent_sync_params(a);
     return RL_OK;
 }
@@ -1694,6 +1961,7 @@ int rl_agent_set_delta_buffer(rl_agent *a, void *ptr, uint64_t n_words) {
 int rl_agent_set_merge_groups(rl_agent *a, uint64_t total_groups) {
     if (!a) return fail(RL_E_ARG, "null agent");
     a->merge_groups = total_groups ? total_groups : a->n_groups;
+    a->merge_groups_set = true;
     return RL_OK;
 }
 
@@ -1706,6 +1974,11 @@ int rl_agent_launch_train(rl_agent *a) {
 int rl_agent_launch_fold(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
+    // an external collective must declare the learner groups of every rank: the
+    // f64 grid's headroom depends on it
+    if (a->delta_max != a->delta_own && !a->comm && !a->merge_groups_set && a->qrepr == RL_QREPR_F64)
+        return fail(RL_E_STATE, "external merge buffer: call rl_agent_set_merge_groups with the total learner "
+                                "groups over every rank first");
     return launch_fold_kernel(a);
 }
 
@@ -1748,7 +2021,35 @@ void rl_comm_destroy(rl_comm *c) {
     (void)hipSetDevice(c->device);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->word) (void)hipFree(c->word);
+    if (c->vals) (void)hipFree(c->vals);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+int rl_comm_allreduce_f64(rl_comm *c, double *vals, uint32_t n, int32_t op) {
+    if (!c || (!vals && n) || op < 0 || op > 2) return fail(RL_E_ARG, "bad argument");
+    if (!c->comm) return fail(RL_E_STATE, "communicator aborted after a fatal error on this rank");
+    HIPC(hipSetDevice(c->device));
+    if (!c->stream) HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (n > c->n_vals) {
+        if (c->vals) HIPC(hipFree(c->vals));
+        c->vals = nullptr;
+        c->n_vals = 0;
+        HIPC(hipMalloc((void **)&c->vals, (size_t)n * 8));
+        c->n_vals = n;
+    }
+    const ncclRedOp_t rop = op == 0 ? ncclSum : (op == 1 ? ncclMax : ncclMin);
+    // n == 0 is a barrier: one word all-reduced, nothing copied back
+    const uint32_t m = n ? n : 1;
+    if (!c->vals) {
+        HIPC(hipMalloc((void **)&c->vals, 8));
+        c->n_vals = 1;
+    }
+    if (n) HIPC(hipMemcpyAsync(c->vals, vals, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    NCCLC(ncclAllReduce(c->vals, c->vals, m, ncclFloat64, rop, c->comm, c->stream));
+    if (n) HIPC(hipMemcpyAsync(vals, c->vals, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return RL_OK;
 }
 
 int rl_comm_rank(rl_comm *c, int32_t *rank, int32_t *world) {
@@ -1771,6 +2072,7 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
         if (rc) return rc;
     }
     a->merge_groups = total;
+    a->merge_groups_set = c != nullptr;
     return RL_OK;
 }
 

@@ -36,8 +36,23 @@ constexpr uint32_t LF_DFLAG = 1u << 10;   // DoubleTabularPolicy::policy_flag (s
 constexpr int LF_MODE_SHIFT = 12;         // rl_lane_mode, 2 bits
 // lane aux record (uint4): x,y = epsilon (f64 bits), z = eval episodes left, w = episode length
 
+// per-call Agent surface (rl_agent_get_action / rl_agent_update): device arrays
+// of call_n entries, entry i for lane call_lane0 + i (dense states)
+enum { CALL_NONE = 0, CALL_GET_ACTION = 1, CALL_UPDATE = 2 };
+struct AgentCall {
+    const uint32_t *s, *a, *s2, *a2;
+    const double *r;
+    const uint8_t *term;
+    uint32_t *action_out;
+    double *td_out;
+};
+
 struct KParams {
     uint32_t L, G, K, S, A, P;
+    // per-call Agent surface (private mode): CALL_NONE for the training launches
+    int32_t call_op;
+    uint32_t call_lane0, call_n;
+    AgentCall call;
     // lanes
     uint4 *core;
     uint4 *rng;
@@ -47,11 +62,14 @@ struct KParams {
     int64_t *q_base;       // [P][S][A]: fixed-point raw words, or f64 bits (fq)
     uint64_t *n_base;      // [S][A] UCB visit counts (u128 in the reference; u64 never wraps in practice)
     uint64_t *t_base;      // [1]
-    int64_t *delta;        // the merge's SUM words: [P*S*A dq][P*S*A group counts][S*A dn][1 dt][3][P*S*A flag counts]
-    int64_t *delta_max;    // the merge's MAX words (f64: per-entry max code over the changed groups) [P*S*A]
+    int64_t *delta;        // the merge's SUM words: fixed point [P*S*A dq][P*S*A group counts][S*A dn][1 dt];
+                           // f64 [psal grid sums][psal group counts][S*A dn][1 dt][3][psal kind counts]
+    int64_t *delta_max;    // the merge's MAX words (f64: per-entry max code over the changed groups) [psal];
+                           // the fixed point has none (delta == delta_max)
     int64_t *delta_rep;    // n_rep replicas of `delta`: group g adds into replica g % n_rep
     uint32_t n_rep;        // (spreads the same-address int64 atomics of the merge)
-    uint32_t delta_words;
+    uint32_t delta_words;  // replica stride (dense layout)
+    uint32_t sum_words;    // SUM words in use: fixed point 2*PSA + SA + 1, f64 5*psal + SA + 1
     // f64 representation (rl_device.h "f64 shared Q"): every group writes its
     // final Q (LDS order, psal entries) to qslot[group][psal] for the merge
     int32_t fq;            // 1: shared Q is f64 (else the proven fixed point)

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_fold_replicas(KParams p) {
     const uint32_t lw = threadIdx.x & 63u, g = threadIdx.x >> 6;
     const uint64_t w = (uint64_t)blockIdx.x * 64u + lw;
     uint64_t s = 0;
-    if (w < p.delta_words) {
+    if (w < p.sum_words) {
         int64_t *x = p.delta_rep + (uint64_t)g * p.delta_words + w;
         const uint64_t stride = 4ull * p.delta_words;
         const uint32_t n = p.n_rep > g ? (p.n_rep - g + 3u) / 4u : 0u;
@@ -130,11 +130,11 @@ __global__ void __launch_bounds__(256) k_fold_replicas(KParams p) {
     }
     part[g][lw] = s;
     __syncthreads();
-    if (g == 0 && w < p.delta_words)
+    if (g == 0 && w < p.sum_words)
         p.delta[w] = (int64_t)((uint64_t)p.delta[w] + part[0][lw] + part[1][lw] + part[2][lw] + part[3][lw]);
 }
 void launch_fold_replicas(const KParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_fold_replicas, dim3((p.delta_words + 63) / 64), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_fold_replicas, dim3((p.sum_words + 63) / 64), dim3(256), 0, s, p);
 }
 
 // ---------------------------------------------------------------- fused fold + apply
@@ -221,6 +221,11 @@ void launch_apply(const KParams &p, hipStream_t s) {
 // Across ranks: MAX all-reduce between a and b, SUM all-reduce between b and apply.
 // Grid: (entry blocks of 64) x (group blocks of 64); 256 threads = 64 entries x
 // 4 group slices of 16 groups.
+// The merge buffer is indexed by the LDS entry j (psal entries: Blackjack
+// eps-greedy holds only its 484 non-terminal rows, the only ones an update can
+// write), so the MAX words are [psal] and the SUM words [psal sums][psal counts]
+// [SA dN][1 dt][3 x psal kind counts]: cfg 5's all-reduced merge is 5x smaller
+// than over the 2048 dense rows.  UCB keeps dense rows (psal == P*S*A).
 __device__ __forceinline__ uint32_t fq_dense(const KParams &p, uint32_t j) {   // LDS index -> dense [P][S][A]
     if (p.psal == p.P * p.S * p.A) return j;
     const uint32_t A = p.A, SAL = BJ_LDS_STATES * A, tbl = j / SAL, r = j - tbl * SAL;
@@ -255,18 +260,18 @@ __global__ void __launch_bounds__(256) k_fq_merge_a(KParams p) {
     code[gs][lw] = c; cnt[gs][lw] = n; kinds[0][gs][lw] = kn; kinds[1][gs][lw] = kp; kinds[2][gs][lw] = km;
     __syncthreads();
     if (gs == 0 && j < p.psal) {
-        const uint32_t i = fq_dense(p, j), PSA = p.P * p.S * p.A;
+        const uint32_t PS = p.psal;
         uint32_t cm = 0, nt = 0, k0 = 0, k1 = 0, k2 = 0;
         for (int q = 0; q < 4; ++q) {
             cm = code[q][lw] > cm ? code[q][lw] : cm;
             nt += cnt[q][lw]; k0 += kinds[0][q][lw]; k1 += kinds[1][q][lw]; k2 += kinds[2][q][lw];
         }
-        if (cm) atomicMax((unsigned long long *)&p.delta_max[i], (unsigned long long)cm);
-        int64_t *d = p.delta, *fc = d + 2 * PSA + p.S * p.A + 1;
-        if (nt) atomicAdd((unsigned long long *)&d[PSA + i], (unsigned long long)nt);
-        if (k0) atomicAdd((unsigned long long *)&fc[i], (unsigned long long)k0);
-        if (k1) atomicAdd((unsigned long long *)&fc[PSA + i], (unsigned long long)k1);
-        if (k2) atomicAdd((unsigned long long *)&fc[2 * PSA + i], (unsigned long long)k2);
+        if (cm) atomicMax((unsigned long long *)&p.delta_max[j], (unsigned long long)cm);
+        int64_t *d = p.delta, *fc = d + 2 * PS + p.S * p.A + 1;
+        if (nt) atomicAdd((unsigned long long *)&d[PS + j], (unsigned long long)nt);
+        if (k0) atomicAdd((unsigned long long *)&fc[j], (unsigned long long)k0);
+        if (k1) atomicAdd((unsigned long long *)&fc[PS + j], (unsigned long long)k1);
+        if (k2) atomicAdd((unsigned long long *)&fc[2 * PS + j], (unsigned long long)k2);
     }
 }
 __global__ void __launch_bounds__(256) k_fq_merge_b(KParams p) {
@@ -274,11 +279,9 @@ __global__ void __launch_bounds__(256) k_fq_merge_b(KParams p) {
     const uint32_t lw = threadIdx.x & 63u, gs = threadIdx.x >> 6;
     const uint32_t j = blockIdx.x * 64u + lw;
     int64_t sum = 0;
-    uint32_t i = 0;
     if (j < p.psal) {
-        i = fq_dense(p, j);
-        const uint64_t base = (uint64_t)p.q_base[i];
-        const int e = fq_grid((uint32_t)p.delta_max[i]) + p.merge_hb;
+        const uint64_t base = (uint64_t)p.q_base[fq_dense(p, j)];
+        const int e = fq_grid((uint32_t)p.delta_max[j]) + p.merge_hb;
         const uint32_t g0 = blockIdx.y * 64u + gs * 16u;
 #pragma unroll 4
         for (uint32_t g = g0; g < g0 + 16u && g < p.n_groups; ++g) {
@@ -291,34 +294,41 @@ __global__ void __launch_bounds__(256) k_fq_merge_b(KParams p) {
     __syncthreads();
     if (gs == 0 && j < p.psal) {
         const int64_t t = part[0][lw] + part[1][lw] + part[2][lw] + part[3][lw];
-        if (t) atomicAdd((unsigned long long *)&p.delta[i], (unsigned long long)t);
+        if (t) atomicAdd((unsigned long long *)&p.delta[j], (unsigned long long)t);
     }
 }
+// Q_base = the merged value of every entry some group changed.  The grid sums are
+// exact only while the changed groups (over every rank) number at most
+// 2^(10 + merge_hb) (rl_host.cpp merge_headroom); a larger count — an external
+// collective over more groups than rl_agent_set_merge_groups declared — is counted
+// in rl_stats.delta_saturations, and train / evaluate fail on it.
 __global__ void k_fq_apply(KParams p) {
-    const uint32_t PSA = p.P * p.S * p.A, SA = p.S * p.A;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t *d = p.delta, *fc = d + 2 * PSA + SA + 1;
-    if (i < PSA) {
-        const uint64_t n = (uint64_t)d[PSA + i];
+    const uint32_t PS = p.psal, SA = p.S * p.A;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t *d = p.delta, *fc = d + 2 * PS + SA + 1;
+    if (j < PS) {
+        const uint64_t n = (uint64_t)d[PS + j];
         if (n) {
-            const uint32_t f = (fc[i] ? QF_NAN : 0u) | (fc[PSA + i] ? QF_PINF : 0u) | (fc[2 * PSA + i] ? QF_NINF : 0u);
+            const uint32_t f = (fc[j] ? QF_NAN : 0u) | (fc[PS + j] ? QF_PINF : 0u) | (fc[2 * PS + j] ? QF_NINF : 0u);
             double v;
             if (f) v = nf_value(f);
-            else v = __builtin_ldexp((double)d[i] * (1.0 / (double)n), fq_grid((uint32_t)p.delta_max[i]) + p.merge_hb);
-            p.q_base[i] = (int64_t)f64_bits(canon_nan(v));
+            else v = __builtin_ldexp((double)d[j] * (1.0 / (double)n), fq_grid((uint32_t)p.delta_max[j]) + p.merge_hb);
+            p.q_base[fq_dense(p, j)] = (int64_t)f64_bits(canon_nan(v));
+            if (n > (1ull << (10 + p.merge_hb)))
+                atomicAdd(&p.stats[(blockIdx.x % STATS_REP) * STATS_W + ACC_SAT], 1ull);
         }
-        d[i] = 0;
-        d[PSA + i] = 0;
-        fc[i] = fc[PSA + i] = fc[2 * PSA + i] = 0;
-        p.delta_max[i] = 0;
+        d[j] = 0;
+        d[PS + j] = 0;
+        fc[j] = fc[PS + j] = fc[2 * PS + j] = 0;
+        p.delta_max[j] = 0;
     }
-    if (i < SA) {
-        p.n_base[i] = p.n_base[i] + (uint64_t)d[2 * PSA + i];
-        d[2 * PSA + i] = 0;
+    if (j < SA) {
+        p.n_base[j] = p.n_base[j] + (uint64_t)d[2 * PS + j];
+        d[2 * PS + j] = 0;
     }
-    if (i == 0) {
-        p.t_base[0] = (uint64_t)((int64_t)p.t_base[0] + d[2 * PSA + SA]);
-        d[2 * PSA + SA] = 0;
+    if (j == 0) {
+        p.t_base[0] = (uint64_t)((int64_t)p.t_base[0] + d[2 * PS + SA]);
+        d[2 * PS + SA] = 0;
     }
 }
 void launch_fq_merge_a(const KParams &p, hipStream_t s) {
@@ -328,8 +338,8 @@ void launch_fq_merge_b(const KParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_fq_merge_b, dim3((p.psal + 63) / 64, (p.n_groups + 63) / 64), dim3(256), 0, s, p);
 }
 void launch_fq_apply(const KParams &p, hipStream_t s) {
-    const uint32_t PSA = p.P * p.S * p.A;
-    hipLaunchKernelGGL(k_fq_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p);
+    const uint32_t n = p.psal > p.S * p.A ? p.psal : p.S * p.A;
+    hipLaunchKernelGGL(k_fq_apply, dim3((n + 255) / 256), dim3(256), 0, s, p);
 }
 
 // ---------------------------------------------------------------- batched Env trait

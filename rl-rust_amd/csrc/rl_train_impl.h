@@ -1867,25 +1867,38 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     flush_stats(p, L, C, active, ACC);
 }
 
-// one private lane (a whole reference agent) for K synchronous steps
+// One private lane as a reference agent: Policy + ActionSelection + the TD update,
+// over the lane's f64 Q / UCB counters / trace set / network in HBM.  Used by the
+// private training kernel (K steps per launch) and by the per-call Agent surface
+// (k_agent_call: rl_agent_get_action / rl_agent_update).
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
-__device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
-                                                 LaneRegs &L, Counters &C) {
+struct PrivAgent {
     using E = EnvDev<ENV>;
-    constexpr int A = E::A;
-    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
-    constexpr bool UCB = SEL == RL_SEL_UCB;
-    constexpr bool NEURAL = POLICY == RL_POLICY_NEURAL;
-    const uint32_t SA = p.S * (uint32_t)A;
-    const uint64_t Ls = p.L;
-    uint64_t t = UCB ? p.t_priv[lane] : 0;
-    uint32_t tcnt = AGENT == RL_AGENT_TRACES ? p.tcnt[lane] : 0u;
-    const NetLane net{p.net_w, Ls, lane, p.n_in, p.n_hidden, (uint32_t)A};
+    static constexpr int A = E::A;
+    static constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    static constexpr bool UCB = SEL == RL_SEL_UCB;
+    static constexpr bool NEURAL = POLICY == RL_POLICY_NEURAL;
+    const KParams &p;
+    const uint64_t lane, Ls;
+    const uint32_t SA;
+    LaneRegs &L;
+    Counters &C;
+    uint64_t t;        // UCB t (upper_confidence_bound.rs:13)
+    uint32_t tcnt;     // traces: visited states this episode
+    const NetLane net;
     NetCache<A> nc;
 
-    auto qref = [&](uint32_t idx) -> double & { return p.q_priv[(uint64_t)idx * Ls + lane]; };
+    __device__ __forceinline__ PrivAgent(const KParams &p_, uint64_t lane_, LaneRegs &L_, Counters &C_)
+        : p(p_), lane(lane_), Ls(p_.L), SA(p_.S * (uint32_t)A), L(L_), C(C_),
+          t(UCB ? p_.t_priv[lane_] : 0), tcnt(AGENT == RL_AGENT_TRACES ? p_.tcnt[lane_] : 0u),
+          net{p_.net_w, p_.L, lane_, p_.n_in, p_.n_hidden, (uint32_t)A} {}
+    __device__ __forceinline__ void store() {
+        if (UCB) p.t_priv[lane] = t;
+        if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
+    }
+    __device__ __forceinline__ double &qref(uint32_t idx) const { return p.q_priv[(uint64_t)idx * Ls + lane]; }
     // Policy::predict (tabular_policy.rs:27-29, double_tabular_policy.rs:31-40, neural_policy.rs:43-47)
-    auto predict = [&](uint32_t s, double (&v)[A]) {
+    __device__ __forceinline__ void predict(uint32_t s, double (&v)[A]) {
         if constexpr (NEURAL) {
             nc.get(p, net, s);
 #pragma unroll
@@ -1897,27 +1910,27 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             if constexpr (P == 1) v[i] = qref(s * A + i);
             else v[i] = (qref(s * A + i) + qref(SA + s * A + i)) / 2.0;
         }
-    };
+    }
     // Policy::get_values of table `tbl` (double policy: flag ? alpha : beta)
-    auto values = [&](uint32_t tbl, uint32_t s, double (&v)[A]) {
+    __device__ __forceinline__ void values(uint32_t tbl, uint32_t s, double (&v)[A]) {
         if constexpr (NEURAL) {
             predict(s, v);
         } else {
 #pragma unroll
             for (int i = 0; i < A; ++i) v[i] = qref(tbl * SA + s * A + i);
         }
-    };
+    }
     // Policy::update with x = td (one-step) or td * E[o][b] (traces)
-    auto pol_update = [&](uint32_t tbl, uint32_t s, uint32_t a, double x) {
+    __device__ __forceinline__ void pol_update(uint32_t tbl, uint32_t s, uint32_t a, double x) {
         if constexpr (NEURAL) {
             net_policy_update<A>(p, net, nc, s, a, x);
         } else {
             double &q = qref(tbl * SA + s * A + a);             // tabular_policy.rs:36
             q = q + p.lr * x;
         }
-    };
-    // get_action with the reference's immediate UCB increments
-    auto select = [&](uint32_t s) -> uint32_t {
+    }
+    // Agent::get_action (one_step_agent.rs:48-51) with the reference's immediate UCB increments
+    __device__ __forceinline__ uint32_t select(uint32_t s) {
         double v[A];
         predict(s, v);
         if constexpr (!UCB) {
@@ -1934,10 +1947,10 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             t += 1;
             return a;
         }
-    };
+    }
     // Agent::update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
     // against the lane's current Q, with after_update and the termination hooks
-    auto update = [&](uint32_t s, uint32_t a, double r, bool term, uint32_t s2, uint32_t a2) -> double {
+    __device__ __forceinline__ double update(uint32_t s, uint32_t a, double r, bool term, uint32_t s2, uint32_t a2) {
         const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;
         const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;
         double q2[A], pr[A];
@@ -1983,8 +1996,46 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         if (P == 2) L.dflag = !L.dflag;                        // after_update
         if constexpr (!UCB) { if (term) L.eps = decay_eps(p, L.eps); }
         return td;
-    };
+    }
+    // the training update as the agent's own update() does it: the inner agent's,
+    // then for InternalModelAgent (src/agent/internal_model_agent.rs:47-77)
+    // model.add_info, which keeps the first (s', r) seen for (s, a)
+    // (random_model.rs:34-38), and planning_steps replays of a uniformly drawn
+    // entry (gen_range, :29-31) through get_action + update(terminated = false)
+    __device__ __forceinline__ double train_update(uint32_t s, uint32_t a, double r, bool term, uint32_t s2,
+                                                   uint32_t a2) {
+        const double td = update(s, a, r, term, s2, a2);
+        if (p.plan_steps) {
+            uint32_t mc = p.mcnt[lane];
+            const uint32_t key = s * A + a;
+            const uint32_t j0 = p.mslot[(uint64_t)key * Ls + lane];
+            if (!(j0 < mc && p.mkey[(uint64_t)j0 * Ls + lane] == key)) {
+                p.mkey[(uint64_t)mc * Ls + lane] = key;
+                p.ms2[(uint64_t)mc * Ls + lane] = s2;
+                p.mr[(uint64_t)mc * Ls + lane] = r;
+                p.mslot[(uint64_t)key * Ls + lane] = mc;
+                ++mc;
+                p.mcnt[lane] = mc;
+            }
+            for (uint32_t i = 0; i < p.plan_steps; ++i) {
+                const uint32_t j = gen_index(L.rng, mc);
+                const uint32_t pk = p.mkey[(uint64_t)j * Ls + lane];
+                const uint32_t ps2 = p.ms2[(uint64_t)j * Ls + lane];
+                const double pr = p.mr[(uint64_t)j * Ls + lane];
+                const uint32_t na = select(ps2);
+                update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
+            }
+        }
+        return td;
+    }
+};
 
+// one private lane (a whole reference agent) for K synchronous steps
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
+                                                 LaneRegs &L, Counters &C) {
+    using E = EnvDev<ENV>;
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C);
     for (uint32_t k = 0; k < p.K; ++k) {
         if (L.mode == RL_MODE_DONE) {
             if (p.rec) write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
@@ -1993,7 +2044,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         if (L.need_reset) {                       // RESET step: src/agent.rs:83-84
             L.s = E::reset(L.z, L.rng, tabs);
             L.ready = true;
-            L.a = select(L.s);
+            L.a = ag.select(L.s);
             L.need_reset = false;
             L.epi_reward = 0.0;
             L.epi_len = 0;
@@ -2009,35 +2060,10 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
-        const uint32_t a2 = select(s2);
+        const uint32_t a2 = ag.select(s2);
         double td = 0.0;
         if (L.mode == RL_MODE_TRAIN) {
-            td = update(L.s, L.a, r, term, s2, a2);
-            if (p.plan_steps) {
-                // InternalModelAgent (src/agent/internal_model_agent.rs:47-77): model.add_info
-                // keeps the first (s', r) seen for (s, a) (random_model.rs:34-38), then
-                // planning_steps replays of a uniformly drawn entry (gen_range, :29-31)
-                // through get_action + update(terminated = false)
-                uint32_t mc = p.mcnt[lane];
-                const uint32_t key = L.s * A + L.a;
-                const uint32_t j0 = p.mslot[(uint64_t)key * Ls + lane];
-                if (!(j0 < mc && p.mkey[(uint64_t)j0 * Ls + lane] == key)) {
-                    p.mkey[(uint64_t)mc * Ls + lane] = key;
-                    p.ms2[(uint64_t)mc * Ls + lane] = s2;
-                    p.mr[(uint64_t)mc * Ls + lane] = r;
-                    p.mslot[(uint64_t)key * Ls + lane] = mc;
-                    ++mc;
-                    p.mcnt[lane] = mc;
-                }
-                for (uint32_t i = 0; i < p.plan_steps; ++i) {
-                    const uint32_t j = gen_index(L.rng, mc);
-                    const uint32_t pk = p.mkey[(uint64_t)j * Ls + lane];
-                    const uint32_t ps2 = p.ms2[(uint64_t)j * Ls + lane];
-                    const double pr = p.mr[(uint64_t)j * Ls + lane];
-                    const uint32_t na = select(ps2);
-                    update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
-                }
-            }
+            td = ag.train_update(L.s, L.a, r, term, s2, a2);
             C.n_train++;
         } else {
             C.n_eval++;
@@ -2051,8 +2077,33 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
         C.rsum += tr ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : (int64_t)0;
     }
     lane_store(p, lane, L);
-    if (UCB) p.t_priv[lane] = t;
-    if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
+    ag.store();
+}
+
+// The per-call Agent surface (trait Agent, src/agent.rs:52-62) on private lanes
+// [call_lane0, call_lane0 + call_n): CALL_GET_ACTION runs get_action(s) (the
+// selector's draws come from the lane's stream, which the lane's Env view shares:
+// one stream per lane, as thread_rng is one per thread), CALL_UPDATE runs
+// update(s, a, r, term, s2, a2) and returns the TD error.  One thread per lane;
+// the lane's record is read and written back around the call.
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__global__ void __launch_bounds__(256) k_agent_call(KParams p) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.call_n) return;
+    const uint64_t lane = (uint64_t)p.call_lane0 + i;
+    if (lane >= p.L) return;
+    LaneRegs L;
+    Counters C;
+    lane_load(p, lane, true, L);
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C);
+    const AgentCall &c = p.call;
+    if (p.call_op == CALL_GET_ACTION) {
+        c.action_out[i] = ag.select(c.s[i]);
+    } else {
+        c.td_out[i] = ag.train_update(c.s[i], c.a[i], c.r[i], c.term[i] != 0, c.s2[i], c.a2[i]);
+    }
+    lane_store(p, lane, L);
+    ag.store();
 }
 
 // ---------------------------------------------------------------- launch table
@@ -2061,6 +2112,12 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
     const bool instr = p.rec != nullptr || p.elog != nullptr;
     const void *k = nullptr;
     if constexpr (PRIV) {
+        if (p.call_op != CALL_NONE) {   // per-call Agent surface: one thread per lane, no LDS
+            if (occ) { *occ = 0; return hipSuccess; }
+            void *args[] = {(void *)&p};
+            return hipLaunchKernel((const void *)k_agent_call<ENV, AGENT, POLICY, SEL, ALGO>,
+                                   dim3((p.call_n + 255) / 256), dim3(256), args, 0, stream);
+        }
         k = (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>;
     } else if (instr) {
         k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, true>(p);

@@ -84,6 +84,17 @@ SIGNATURES = {
     "rl_last_error": (C.c_char_p, []),
     "rl_abi_version": (C.c_int, []),
     "rl_build_info": (C.c_char_p, []),
+    "rl_build_id": (C.c_char_p, []),
+    "rl_obs_from_reference": (C.c_int, [C.c_int32, C.c_uint64, _P(C.c_uint32)]),
+    "rl_agent_get_action": (C.c_int, [_V, C.c_uint32, C.c_uint64, _P(C.c_uint32)]),
+    "rl_agent_update": (C.c_int, [_V, C.c_uint32, C.c_uint64, C.c_uint32, C.c_double, C.c_int32, C.c_uint64,
+                                  C.c_uint32, _P(C.c_double)]),
+    "rl_agent_get_actions": (C.c_int, [_V, _V, _V]),
+    "rl_agent_updates": (C.c_int, [_V, _V, _V, _V, _V, _V, _V, _V]),
+    "rl_agent_env": (C.c_int, [_V, _P(_V)]),
+    "rl_env_reset_lane": (C.c_int, [_V, C.c_uint32, _P(C.c_uint64)]),
+    "rl_env_step_lane": (C.c_int, [_V, C.c_uint32, C.c_uint32, _P(C.c_uint64), _P(C.c_double),
+                                   _P(C.c_uint8)]),
     "rl_device_count": (C.c_int, [_P(C.c_int)]),
     "rl_blackjack_obs_id": (C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32]),
     "rl_obs_to_reference": (C.c_uint64, [C.c_int32, C.c_uint32]),
@@ -144,11 +155,32 @@ SIGNATURES = {
     "rl_comm_destroy": (None, [_V]),
     "rl_comm_rank": (C.c_int, [_V, _P(C.c_int32), _P(C.c_int32)]),
     "rl_agent_set_comm": (C.c_int, [_V, _V]),
+    "rl_comm_allreduce_f64": (C.c_int, [_V, _V, C.c_uint32, C.c_int32]),
     "rl_agent_sync": (C.c_int, [_V]),
 }
 COMM_ID_BYTES = 128
 
 _lib = None
+
+
+def source_id():
+    """'src:<16 hex>' of this checkout's library sources, computed as the Makefile's
+    ID_SRCS rule does (sha256 of csrc/*.{h,hip,cpp} sorted, include/rl.h, Makefile):
+    equal to the loaded library's rl_build_id() prefix iff it was built from them"""
+    import glob
+    import hashlib
+    files = sorted(os.path.relpath(f, HERE) for pat in ("csrc/*.h", "csrc/*.hip", "csrc/*.cpp")
+                   for f in glob.glob(os.path.join(HERE, pat)))
+    h = hashlib.sha256()
+    for f in files + [os.path.join("..", "include", "rl.h"), "Makefile"]:
+        with open(os.path.join(HERE, f), "rb") as fh:
+            h.update(fh.read())
+    return "src:" + h.hexdigest()[:16]
+
+
+def build_id():
+    """rl_build_id() of the loaded library: 'src:<16 hex> git:<12 hex>'"""
+    return lib().rl_build_id().decode()
 
 
 def lib():
@@ -237,19 +269,26 @@ def env_table(p):
 class Env:
     """Batched Env<usize, COUNT> (src/env.rs:19-49) on the GPU."""
 
-    def __init__(self, p, n_envs=1, seed=0x5EED, lane_offset=0, device=0):
+    def __init__(self, p, n_envs=1, seed=0x5EED, lane_offset=0, device=0, _view_of=None):
         self.p = p
         self.n = n_envs
         self.S, self.A = env_dims(p)
         self.cfg = env_config(p)
         h = C.c_void_p()
-        check(lib().rl_env_create(C.byref(self.cfg), n_envs, seed, lane_offset, device, C.byref(h)))
+        if _view_of is not None:     # Agent.env(): the agent's own lanes and RNG streams
+            check(lib().rl_agent_env(_view_of.h, C.byref(h)))
+            self._agent = _view_of
+        else:
+            check(lib().rl_env_create(C.byref(self.cfg), n_envs, seed, lane_offset, device, C.byref(h)))
         self.h = h
 
-    def __del__(self):
+    def close(self):
         if getattr(self, "h", None):
             lib().rl_env_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        self.close()
 
     def action_size(self):
         return self.A
@@ -258,6 +297,18 @@ class Env:
         obs = np.zeros(self.n, np.uint64)
         check(lib().rl_env_reset(self.h, obs.ctypes.data))
         return obs
+
+    def reset_lane(self, lane):
+        """Env::reset of one lane's env"""
+        o = C.c_uint64()
+        check(lib().rl_env_reset_lane(self.h, lane, C.byref(o)))
+        return o.value
+
+    def step_lane(self, lane, action):
+        """Env::step of one lane's env: (obs, reward, terminated)"""
+        o, r, t = C.c_uint64(), C.c_double(), C.c_uint8()
+        check(lib().rl_env_step_lane(self.h, lane, int(action), C.byref(o), C.byref(r), C.byref(t)))
+        return o.value, r.value, bool(t.value)
 
     def step(self, actions):
         a = np.ascontiguousarray(actions, dtype=np.uint32)
@@ -285,12 +336,50 @@ class Agent:
         self.private = p["group_size"] == 1
 
     def close(self):
+        v = getattr(self, "_env_view", None)
+        if v is not None:
+            v.close()
+            self._env_view = None
         if getattr(self, "h", None):
             lib().rl_agent_destroy(self.h)
             self.h = None
 
     def __del__(self):
         self.close()
+
+    # ---- the per-call Agent surface (trait Agent, src/agent.rs:52-62); private mode
+    def env(self):
+        """Env over this agent's lanes (rl_agent_env): one env per lane, drawing from
+        the lane's RNG stream as the reference's thread_rng serves env and agent"""
+        if getattr(self, "_env_view", None) is None:
+            self._env_view = Env(self.p, self.L, _view_of=self)
+        return self._env_view
+
+    def get_action(self, obs, lane=0):
+        a = C.c_uint32()
+        check(lib().rl_agent_get_action(self.h, lane, int(obs), C.byref(a)))
+        return a.value
+
+    def update(self, curr_obs, curr_action, reward, terminated, next_obs, next_action, lane=0):
+        td = C.c_double()
+        check(lib().rl_agent_update(self.h, lane, int(curr_obs), int(curr_action), float(reward),
+                                    int(bool(terminated)), int(next_obs), int(next_action), C.byref(td)))
+        return td.value
+
+    def get_actions(self, obs):
+        obs = np.ascontiguousarray(obs, np.uint64)
+        out = np.zeros(self.L, np.uint32)
+        check(lib().rl_agent_get_actions(self.h, obs.ctypes.data, out.ctypes.data))
+        return out
+
+    def updates(self, s, a, r, term, s2, a2):
+        s, s2 = np.ascontiguousarray(s, np.uint64), np.ascontiguousarray(s2, np.uint64)
+        a, a2 = np.ascontiguousarray(a, np.uint32), np.ascontiguousarray(a2, np.uint32)
+        r, term = np.ascontiguousarray(r, np.float64), np.ascontiguousarray(term, np.uint8)
+        td = np.zeros(self.L, np.float64)
+        check(lib().rl_agent_updates(self.h, s.ctypes.data, a.ctypes.data, r.ctypes.data, term.ctypes.data,
+                                     s2.ctypes.data, a2.ctypes.data, td.ctypes.data))
+        return td
 
     def set_future_q_value_func(self, algo):
         check(lib().rl_agent_set_future_q_value_func(self.h, ALGO[algo]))
@@ -504,6 +593,15 @@ class Comm:
         check(lib().rl_comm_init(rank, world, buf, device, C.byref(h)))
         self.h = h
         self.rank, self.world = rank, world
+
+    def allreduce(self, vals, op="sum"):
+        """host values all-reduced over the ranks (RCCL): op sum / max / min"""
+        x = np.ascontiguousarray(np.atleast_1d(vals), np.float64).copy()
+        check(lib().rl_comm_allreduce_f64(self.h, x.ctypes.data, x.size, {"sum": 0, "max": 1, "min": 2}[op]))
+        return x
+
+    def barrier(self):
+        check(lib().rl_comm_allreduce_f64(self.h, None, 0, 0))
 
     def close(self):
         if getattr(self, "h", None):

@@ -36,9 +36,28 @@ def test_library_exports_every_declared_symbol(rl):
     assert not missing, missing
     # and the Python binding covers the whole header
     assert set(names) <= set(rl.SIGNATURES), set(names) - set(rl.SIGNATURES)
-    assert rl.lib().rl_abi_version() == 4
+    assert rl.lib().rl_abi_version() == 5
     info = rl.lib().rl_build_info().decode()
     assert "gfx950" in info and "RLAMD_EXP=0" in info and "-ffp-contract=off" in info, info
+
+
+def test_loaded_library_was_built_from_this_checkout(rl):
+    """rl_build_id's source hash == the hash of the sources in this tree, so a stale
+    librlamd.so (built from other sources) fails here instead of being benched or
+    profiled unnoticed"""
+    bid = rl.build_id()
+    assert bid.startswith("src:") and " git:" in bid, bid
+    assert bid.split()[0] == rl.source_id(), (bid, rl.source_id(), "rebuild: make -C rl-rust_amd")
+    assert bid in rl.lib().rl_build_info().decode()
+
+
+def test_obs_from_reference_inverts_obs_to_reference(rl):
+    L = rl.lib()
+    d = ctypes.c_uint32()
+    for s in range(2048):
+        assert L.rl_obs_from_reference(3, L.rl_obs_to_reference(3, s), ctypes.byref(d)) == 0 and d.value == s
+    assert L.rl_obs_from_reference(3, 12345, ctypes.byref(d)) == 2
+    assert L.rl_obs_from_reference(2, 499, ctypes.byref(d)) == 0 and d.value == 499
 
 
 ENV_CASES = [("frozen_lake_4x4_det", dict(env="frozen_lake", map8x8=0, slippery=0)),
