@@ -460,6 +460,16 @@ __device__ __forceinline__ double nf_value(uint32_t f) {
 __device__ __forceinline__ int64_t fq_raw(double d, int e) {
     return (int64_t)__builtin_rint(__builtin_ldexp(d, -e));
 }
+// 1.0 / n (0 for n == 0) without a table read: v_rcp_f64 and one Newton step.
+// Correctly rounded for every n the kernels use (n <= 1024 contributions): checked
+// against the IEEE division for n = 0 .. 65535 on the device (rl_kat_rcp,
+// tests/test_gpu_parity.py::test_kat_rcp_newton)
+__device__ __forceinline__ double rcp_nr(uint32_t n) {
+    const double dn = (double)n;
+    const double r0 = __builtin_amdgcn_rcp(dn);
+    const double e = __builtin_fma(-dn, r0, 1.0);
+    return n ? __builtin_fma(r0, e, r0) : 0.0;
+}
 // argmax (first maximum, strict >) and max of one f64 row in a single pass
 // (utils.rs:1-21: a NaN at index 0 sticks, later NaNs never win)
 template <int A>

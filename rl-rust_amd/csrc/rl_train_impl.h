@@ -13,6 +13,8 @@
 //                   with f64 Q / UCB counters in HBM (SoA [entry][lane]) — the
 //                   reference's arithmetic bit for bit.
 #pragma once
+#include <type_traits>
+
 #include "rl_device.h"
 #include "rl_net.h"
 
@@ -24,7 +26,7 @@ namespace rlamd {
 #endif
 
 struct SmemLayout {
-    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, qd, total;
+    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, qd, rm, total;
     uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
@@ -84,6 +86,24 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 __host__ __device__ constexpr bool qsh_layout(int fq, int ucb, int P, int algo) {
     return RLAMD_QSH != 0 && RLAMD_FUSE_MAX != 0 && !fq && !ucb && P == 1 && algo == RL_ALGO_QLEARNING;
 }
+// Row summaries (the QSH layout, rows of 4 actions): RM[s] = (max, argmax) of row
+// s, written by the settle for every row each step, so a step reads its target
+// row's argmax (the exploit action) and max (the Q-learning target) as one 16-byte
+// LDS read instead of the 32-byte row and the 4-way compare chain.  The settle
+// then runs on 2 of a group's 8 waves, each thread two entries of a row, with the
+// row's halves combined across lane pairs (DPP).
+#ifndef RLAMD_ROWMAX
+#define RLAMD_ROWMAX 1
+#endif
+#ifndef RLAMD_RM_PIN
+#define RLAMD_RM_PIN 0
+#endif
+#ifndef RLAMD_SETTLE_RCPN
+#define RLAMD_SETTLE_RCPN 0   // 1: the settle's 1/n by v_rcp_f64 + one Newton step, no table read
+#endif
+#ifndef RLAMD_SETTLE_QUAD
+#define RLAMD_SETTLE_QUAD 1   // 1: one entry per thread (4 waves), the row summary by 2 DPP steps per quad
+#endif
 // LDS carve of one learner group (shared mode) or of the tables only (private).
 //   misc u32[4]            f64 traces: the group step's max td code
 //   q    int64 [P][S][A]   the group's Q copy (fixed point 2^-40, or f64 bits)
@@ -161,6 +181,8 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     //                    entry beside its int64 word (qsh_layout), read by the step
     if (shared_q && qsh) off = align16(off);
     l.qd = off; off += (shared_q && qsh) ? PSA * 8u : 0u;
+    off = align16(off);
+    l.rm = off; off += (shared_q && qsh && RLAMD_ROWMAX && A == 4u && P == 1) ? SL * 16u : 0u;
     l.total = off;
     return l;
 }
@@ -257,6 +279,9 @@ __device__ __forceinline__ bool eval_hit(const KParams &p, uint32_t ep) {
 // different steps, and the branchy form was mis-scheduled at -O3 (a lost
 // train_ep increment, caught by the parity tests).
 // Sets tr / ev when a training / evaluation episode ended (the caller counts them).
+// EPI: 0 = throughput mode compiled in (no target, no eval interleave: rl_agent_run),
+// 1 = episodic, -1 = KParams::episodic at run time
+template <int EPI = -1>
 __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32_t s2, uint32_t a2,
                                            double r, bool term, bool &tr_out, bool &ev_out) {
     L.epi_reward += r;
@@ -267,7 +292,7 @@ __device__ __forceinline__ void after_step(const KParams &p, LaneRegs &L, uint32
     const bool ev = term && L.mode == RL_MODE_EVAL;
     tr_out = tr;
     ev_out = ev;
-    if (!p.episodic) {   // throughput mode (rl_agent_run): no target, no eval interleave;
+    if (EPI == 0 || (EPI < 0 && !p.episodic)) {   // throughput mode (rl_agent_run): no target, no eval interleave;
         // the general logic below reduces to exactly this
         L.train_ep += tr ? 1u : 0u;
         const uint32_t el = L.eval_left - (ev ? 1u : 0u);
@@ -573,7 +598,7 @@ constexpr bool fix_possible() {
 // FQ: the group's Q is f64 (rl_device.h "f64 shared Q"); else the fixed point,
 // which the host runs only where it proved the range (no clamp can engage).
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, bool FQ, int SLIP = -1, int SWEEP = -1,
-          bool PACK = false, int RS = -1>
+          bool PACK = false, int RS = -1, int EPI = -1>
 __device__ __forceinline__ void train_shared_body(const KParams &p) {
     using E = EnvDev<ENV>;
     constexpr int A = E::A;
@@ -594,6 +619,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                                        nthr, p.trc_kb, FQ ? 1 : 0, p.ucb_pack, QSH ? 1 : 0);
     unsigned long long *Q = (unsigned long long *)(smem + lay.q);
     double *QD = (double *)(smem + lay.qd);              // QSH: f64 images of Q's words
+    double2 *RM = (double2 *)(smem + lay.rm);            // QSH rows of 4: (max, argmax bits) per row
     unsigned long long *SUM = (unsigned long long *)(smem + lay.sum);
     uint32_t *CNT = (uint32_t *)(smem + lay.cnt);        // fixed point: two u16 counters per word
     uint16_t *CNT16 = (uint16_t *)(smem + lay.cnt);
@@ -674,6 +700,18 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     }
     if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
         for (uint32_t i = tid; i < SA; i += nthr) TR[lds_of(i)] = p.trans[i];
+    // row summaries (RLAMD_ROWMAX): in the sweep form only (the settle rewrites them)
+    const bool sweep = SWEEP == 1 || PSAL <= nthr;   // SWEEP == 1: the host checked PSA <= block
+    const bool rmx = QSH && RLAMD_ROWMAX && A == 4 && sweep;
+    if (rmx) {
+        for (uint32_t r = tid; r < SL; r += nthr) {
+            double v[A], m;
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = q_val(p.q_base[r * (uint32_t)A + i]);
+            const uint32_t a = argmax_max_f64<A>(v, m);
+            RM[r] = make_double2(m, as_f64((uint64_t)a));
+        }
+    }
     __syncthreads();
 
     EnvTables tabs;
@@ -895,7 +933,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // (the table fits the block, PSA <= nthr): thread i settles entry i every step,
     // so the counter add needs no return value.  Owner form: the step's first
     // contributor (old count 0) settles the entry.
-    const bool sweep = SWEEP == 1 || PSAL <= nthr;   // SWEEP == 1: the host checked PSA <= block
     // PACKC: one LDS atomic per contribution — SUM[idx] holds sum * 2^11 + count
     // (KParams::pack_ok: the host proved |sum| * 2^11 + 2047 < 2^63)
     constexpr bool PACKC = PACK && !FQ;
@@ -914,11 +951,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     };
     // fixed point owner: Q[idx] += mean of the step's contributions (proven in
     // range: no clamp), clear accumulators
-    auto settle = [&](uint32_t idx) {
+    auto settle = [&](uint32_t idx) -> double {
         const int64_t packed = (int64_t)SUM[idx];
         const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[idx];
         const int64_t sum = PACKC ? (packed >> 11) : packed;
-        const double rc = (sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n;   // sweep: n <= block size
+        const double rc = RLAMD_SETTLE_RCPN ? rcp_nr(n)
+                                            : ((sweep || n < lay.nrcp) ? RCP[n] : 1.0 / (double)n);   // sweep: n <= block size
         // packed: |sum| < 2^51 (pack_proven), so (double)sum is the 1.5*2^52 magic
         const double sd = PACKC ? __longlong_as_double((long long)(0x4338000000000000ull + (uint64_t)sum)) - 0x1.8p52
                                 : (double)sum;
@@ -926,9 +964,74 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         const int64_t md = (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
         const unsigned long long q = Q[idx] + (unsigned long long)md;
         Q[idx] = q;
-        if constexpr (QSH) QD[idx] = q_val((int64_t)q);
+        const double v = q_val((int64_t)q);
+        if constexpr (QSH) QD[idx] = v;
         SUM[idx] = 0ull;
         if constexpr (!PACKC) CNT16[idx] = 0;
+        return v;
+    };
+    // row summaries (rmx): thread t settles entries 2t, 2t + 1 (half t & 1 of row t >> 1)
+    // as settle() does, then the row's (max, argmax) — first maximum, strict > as
+    // argmax_max_f64 — from its half and its partner lane's (t ^ 1, same wave)
+    auto settle_pair = [&](uint32_t t) {
+        const uint32_t j = 2u * t;
+        const ulonglong2 sp = *(const ulonglong2 *)__builtin_assume_aligned(&SUM[j], 16);
+        const ulonglong2 qp = *(const ulonglong2 *)__builtin_assume_aligned(&Q[j], 16);
+        int64_t md[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t packed = (int64_t)(h ? sp.y : sp.x);
+            const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[j + h];
+            const int64_t sum = PACKC ? (packed >> 11) : packed;
+            const double sd = PACKC ? __longlong_as_double((long long)(0x4338000000000000ull + (uint64_t)sum)) - 0x1.8p52
+                                    : (double)sum;
+            const double rc = RLAMD_SETTLE_RCPN ? rcp_nr(n) : RCP[n];
+            const double y = __builtin_trunc(sd * rc) + 0x1.8p52;
+            md[h] = (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
+        }
+        const unsigned long long q0 = qp.x + (unsigned long long)md[0], q1 = qp.y + (unsigned long long)md[1];
+        *(ulonglong2 *)__builtin_assume_aligned(&Q[j], 16) = make_ulonglong2(q0, q1);
+        const double v0 = q_val((int64_t)q0), v1 = q_val((int64_t)q1);
+        *(double2 *)__builtin_assume_aligned(&QD[j], 16) = make_double2(v0, v1);
+        *(ulonglong2 *)__builtin_assume_aligned(&SUM[j], 16) = make_ulonglong2(0ull, 0ull);
+        if constexpr (!PACKC) *(uint32_t *)&CNT16[j] = 0u;
+        const bool up = v1 > v0;
+        const double m = up ? v1 : v0;
+        const uint32_t a = (t & 1u) * 2u + (up ? 1u : 0u);
+        // the partner half (lanes t, t ^ 1): quad_perm [1,0,3,2]
+        const uint64_t mb = f64_bits(m);
+        const uint32_t pml = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)mb, 0xB1, 0xF, 0xF, false);
+        const uint32_t pmh = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(mb >> 32), 0xB1, 0xF, 0xF, false);
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xB1, 0xF, 0xF, false);
+        const double pm = as_f64(((uint64_t)pmh << 32) | pml);
+        if ((t & 1u) == 0u) {                 // low half: its entries come first (ties stay)
+            const bool hi = pm > m;
+            RM[t >> 1] = make_double2(hi ? pm : m, as_f64((uint64_t)(hi ? pa : a)));
+        }
+    };
+    // RLAMD_SETTLE_QUAD: thread t settles entry t (row t >> 2 is one lane quad) and
+    // the row summary comes from two DPP combines (pairs, then pairs of pairs; the
+    // lower entries win ties, as argmax_max_f64's strict >)
+    auto settle_quad = [&](uint32_t t) {
+        double m = settle(t);
+        uint32_t a = t & 3u;
+        auto combine = [&](auto dpp_ctrl_tag, uint32_t bit) {
+            constexpr int C = decltype(dpp_ctrl_tag)::value;
+            const uint64_t mb = f64_bits(m);
+            const uint32_t pl = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)mb, C, 0xF, 0xF, false);
+            const uint32_t ph = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(mb >> 32), C, 0xF, 0xF, false);
+            const uint32_t pa = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, C, 0xF, 0xF, false);
+            const double pm = as_f64(((uint64_t)ph << 32) | pl);
+            const bool mine_lo = (t & bit) == 0u;
+            const double lo = mine_lo ? m : pm, hi = mine_lo ? pm : m;
+            const uint32_t la = mine_lo ? a : pa, ha = mine_lo ? pa : a;
+            const bool up = hi > lo;
+            m = up ? hi : lo;
+            a = up ? ha : la;
+        };
+        combine(std::integral_constant<int, 0xB1>{}, 1u);   // quad_perm [1,0,3,2]
+        combine(std::integral_constant<int, 0x4E>{}, 2u);   // quad_perm [2,3,0,1]
+        if ((t & 3u) == 0u) RM[t >> 2] = make_double2(m, as_f64((uint64_t)a));
     };
     // f64 owner: the entry moves by the mean of the step's contributions on their
     // grid (or by the IEEE result of its non-finite ones), NaN canonical
@@ -1036,9 +1139,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             for (int i = 0; i < A; ++i) v[i] = as_f64(ra2[i]);
                             pre = (int32_t)argmax_max_f64<A>(v, m);
                         } else if constexpr (QSH) {
-                            double v[A], m;
-                            qd_row(s0, v);
-                            pre = (int32_t)argmax_max_f64<A>(v, m);
+                            if (rmx) {
+                                pre = (int32_t)(uint32_t)f64_bits(RM[s0].y);
+                            } else {
+                                double v[A], m;
+                                qd_row(s0, v);
+                                pre = (int32_t)argmax_max_f64<A>(v, m);
+                            }
                         } else {
                             pre = (int32_t)argmax_i64<A>(ra2);
                         }
@@ -1095,7 +1202,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             // and barriers and each ballot re-materialised its mask (2 VALU each)
             c_train += (uint32_t)__popcll(__ballot(train_lane));
             c_tep += (uint32_t)__popcll(__ballot(train_lane && term));
-            if (p.episodic) {
+            if (EPI > 0 || (EPI < 0 && p.episodic)) {
                 const bool ev_lane = doS && L.mode == RL_MODE_EVAL;
                 c_eval += (uint32_t)__popcll(__ballot(ev_lane));
                 c_eep += (uint32_t)__popcll(__ballot(ev_lane && term));
@@ -1106,6 +1213,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
             for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
         }
+        uint32_t rm_pad = 0;                // rmx: the row summary's 4th dword (see below)
         int64_t rmax = 0;                   // FUSE_MAX: utils::max of row s2 (the Q-learning target)
         double rmaxd = 0.0;
         int32_t rarg = -1;
@@ -1117,10 +1225,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
                 if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
             } else if constexpr (QSH) {
-                double v[A];
-                qd_row(s2, v);
-                rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
-                if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
+                if (rmx) {
+                    // no pin: the load's wait can sink to the first use (the exploit
+                    // branch, the TD), past the eps test and the exploring draw.  Its
+                    // unused 4th dword is kept live up to the TD (rm_pad): else the
+                    // compiler reuses that register at once and must wait for the load
+                    const double2 rm = RM[s2];
+                    rmaxd = rm.x;
+                    rarg = (int32_t)(uint32_t)f64_bits(rm.y);
+                    rm_pad = (uint32_t)(f64_bits(rm.y) >> 32);
+                    if constexpr (RLAMD_RM_PIN) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
+                } else {
+                    double v[A];
+                    qd_row(s2, v);
+                    rarg = (int32_t)argmax_max_f64<A>(v, rmaxd);
+                    if constexpr (RLAMD_FUSE_MAX == 2) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
+                }
             } else {
                 rarg = (int32_t)argmax_max_i64<A>(ra2, rmax);
                 // pin both here (empty asm): left alone, the compiler sinks the index into
@@ -1240,6 +1360,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 const uint32_t qidx = qi(vt, L.s, L.a);
                 const double qa = QSH ? QD[qidx] : val((int64_t)Q[qidx]);
                 td = r + p.gamma * fq - qa;
+                if constexpr (QSH && !RLAMD_RM_PIN) asm volatile("" ::"v"(rm_pad));
             }
         }
         if constexpr (!TRACES) {
@@ -1278,7 +1399,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 bool owner = false;
                 if (train) owner = contribute(idx, rint_i64_small(p.lr40 * td), 1u);   // q_fix_inrange(lr * td)
                 __syncthreads();   // all contributions in, all Q reads done
-                if (sweep) { if (tid < PSAL) settle(tid); }
+                if (rmx) {
+                    if constexpr (RLAMD_SETTLE_QUAD) { if (tid < PSAL) settle_quad(tid); }
+                    else { if (tid < PSAL / 2u) settle_pair(tid); }
+                }
+                else if (sweep) { if (tid < PSAL) settle(tid); }
                 else if (owner) settle(idx);
             }
         } else {
@@ -1642,7 +1767,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
             }
             LaneRegs N = L;
-            after_step(p, N, s2, a2, r, term, tr, ev);   // term is false on RESET / idle lanes
+            after_step<EPI>(p, N, s2, a2, r, term, tr, ev);   // term is false on RESET / idle lanes
             const bool act = doS || doR;
             L.epi_reward = doS ? N.epi_reward : (doR ? 0.0 : L.epi_reward);
             L.epi_len = doS ? N.epi_len : (doR ? 0u : L.epi_len);
@@ -1665,7 +1790,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 }
             }
             if (INSTR && p.rec) write_record(p, k, lane, fused ? 3u : 2u, L.s, L.a, s2, a2, r, term, td, mode_before);
-            after_step(p, L, s2, a2, r, term, tr, ev);
+            after_step<EPI>(p, L, s2, a2, r, term, tr, ev);
             // fixed point: the host also proved |episode reward| * 2^16 < 2^51
             // (delta_bound), so rint is the magic add
             if (tr) atomicAdd(RSUM, (unsigned long long)(FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
@@ -1684,7 +1809,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (!RLAMD_EARLY_COUNT) {
             c_train += (uint32_t)__popcll(__ballot(train));
             c_tep += (uint32_t)__popcll(__ballot(tr));
-            if (p.episodic) {              // run(): lanes only train, so no eval steps / episodes
+            if (EPI > 0 || (EPI < 0 && p.episodic)) {   // run(): lanes only train, so no eval steps / episodes
                 c_eval += (uint32_t)__popcll(__ballot(doS && !train));
                 c_eep += (uint32_t)__popcll(__ballot(ev));
             }
@@ -1755,6 +1880,15 @@ template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR, bool FQ
 __global__ void __launch_bounds__(1024) k_train_shared(KParams p) {
     train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, INSTR, FQ>(p);
 }
+// the throughput mode (rl_agent_run) with the episodic bookkeeping compiled out,
+// as k_train_shared_o8<..., EPI = 0>
+#ifndef RLAMD_SHARED_RUNMODE
+#define RLAMD_SHARED_RUNMODE 1
+#endif
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool FQ>
+__global__ void __launch_bounds__(1024) k_train_shared_run(KParams p) {
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, FQ, -1, -1, false, -1, 0>(p);
+}
 // Eligibility traces on the small tables (FrozenLake, CliffWalking: the pair
 // bitmap) in groups of <= 256 lanes, at most 2 groups per CU (cfg 4: 2^17 lanes in
 // 512 groups): 2 waves per SIMD is all the lanes give, so a wave may hold 256
@@ -1773,9 +1907,12 @@ constexpr bool use_w() {
 // cannot be proven for this variant, so the host never asks for it)
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, bool INSTR>
 const void *shared_kernel(const KParams &p) {
-    if (p.fq) return (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, true>;
+    const bool run = RLAMD_SHARED_RUNMODE && !INSTR && !p.episodic;
+    if (p.fq) return run ? (const void *)k_train_shared_run<ENV, AGENT, POLICY, SEL, ALGO, true>
+                         : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, true>;
     if constexpr (fix_possible<AGENT, POLICY, SEL, ALGO>())
-        return (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, false>;
+        return run ? (const void *)k_train_shared_run<ENV, AGENT, POLICY, SEL, ALGO, false>
+                   : (const void *)k_train_shared<ENV, AGENT, POLICY, SEL, ALGO, INSTR, false>;
     return nullptr;
 }
 // Throughput variant at 8 waves per SIMD (<= 64 VGPRs, <= 96 SGPRs) for the
@@ -1787,9 +1924,21 @@ const void *shared_kernel(const KParams &p) {
 #ifndef RLAMD_O8_WAVES
 #define RLAMD_O8_WAVES 8   // waves per SIMD the o8 kernels are compiled for
 #endif
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
+// EPI 0: the throughput mode (rl_agent_run, no episode target or eval interleave)
+// with the episodic bookkeeping compiled out (fewer live scalars in the step loop);
+// -1: either, by KParams::episodic (train / evaluate)
+#ifndef RLAMD_O8_RUNMODE
+#define RLAMD_O8_RUNMODE 1
+#endif
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS, int EPI>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RLAMD_O8_WAVES, RLAMD_O8_WAVES))) k_train_shared_o8(KParams p) {
-    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, MODE == 3, SLIP, SWEEP, MODE == 2, RS>(p);
+    train_shared_body<ENV, AGENT, POLICY, SEL, ALGO, false, MODE == 3, SLIP, SWEEP, MODE == 2, RS, EPI>(p);
+}
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int MODE, int RS>
+const void *o8_epi(const KParams &p) {
+    if (RLAMD_O8_RUNMODE && !p.episodic)
+        return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, MODE, RS, 0>;
+    return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, MODE, RS, -1>;
 }
 // the reset-and-step schedule is compiled into the 8-wave kernels only where it
 // is the measured better schedule (Blackjack, eps-greedy); elsewhere it runs on
@@ -1801,12 +1950,12 @@ constexpr bool o8_has_reset_step() { return ENV == RL_ENV_BLACKJACK && SEL == RL
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP, int RS>
 const void *o8_kernel_rs(const KParams &p) {
     if (p.fq) {
-        if constexpr (ENV == RL_ENV_BLACKJACK) return (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 3, RS>;
+        if constexpr (ENV == RL_ENV_BLACKJACK) return o8_epi<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 3, RS>(p);
         return nullptr;
     }
     if constexpr (fix_possible<AGENT, POLICY, SEL, ALGO>())
-        return p.pack_ok ? (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 2, RS>
-                         : (const void *)k_train_shared_o8<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1, RS>;
+        return p.pack_ok ? o8_epi<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 2, RS>(p)
+                         : o8_epi<ENV, AGENT, POLICY, SEL, ALGO, SLIP, SWEEP, 1, RS>(p);
     return nullptr;
 }
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, int SLIP, int SWEEP>
@@ -2151,11 +2300,23 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
     return hipLaunchKernel(k, grid, block, args, smem, stream);
 }
 
+// RLAMD_ONLY=ag,po,se,al,pr (experiment builds, scripts/build_variant.sh): only this
+// (agent, policy, selector, algorithm, private) instantiation, so a timing variant
+// of one kernel compiles in a minute instead of the whole table's ten
+#ifdef RLAMD_ONLY
+constexpr int kOnly[5] = {RLAMD_ONLY};
+constexpr bool only_ok(int ag, int po, int se, int al, int pr) {
+    return ag == kOnly[0] && po == kOnly[1] && se == kOnly[2] && al == kOnly[3] && pr == kOnly[4];
+}
+#else
+constexpr bool only_ok(int, int, int, int, int) { return true; }
+#endif
 template <int ENV>
 train_launch_fn train_table_entry(int agent, int policy, int sel, int algo, int priv) {
 #define RLAMD_E(AG, PO, SE, AL, PR)                                                                \
-    if (agent == AG && policy == PO && sel == SE && algo == AL && priv == PR)                      \
-        return &launch_train<ENV, AG, PO, SE, AL, PR>;
+    if constexpr (only_ok(AG, PO, SE, AL, PR))                                                     \
+        if (agent == AG && policy == PO && sel == SE && algo == AL && priv == PR)                  \
+            return &launch_train<ENV, AG, PO, SE, AL, PR>;
 #define RLAMD_E1(AG, PO, SE, AL) RLAMD_E(AG, PO, SE, AL, 0) RLAMD_E(AG, PO, SE, AL, 1)
 #define RLAMD_E2(AG, PO, SE)                                                                       \
     RLAMD_E1(AG, PO, SE, RL_ALGO_SARSA) RLAMD_E1(AG, PO, SE, RL_ALGO_QLEARNING)                     \
