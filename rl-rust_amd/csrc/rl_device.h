@@ -460,15 +460,21 @@ __device__ __forceinline__ double nf_value(uint32_t f) {
 __device__ __forceinline__ int64_t fq_raw(double d, int e) {
     return (int64_t)__builtin_rint(__builtin_ldexp(d, -e));
 }
-// 1.0 / n (0 for n == 0) without a table read: v_rcp_f64 and one Newton step.
-// Correctly rounded for every n the kernels use (n <= 1024 contributions): checked
-// against the IEEE division for n = 0 .. 65535 on the device (rl_kat_rcp,
-// tests/test_gpu_parity.py::test_kat_rcp_newton)
+// 1.0 / n (0 for n == 0) without a table read: v_rcp_f64 and two Newton steps
+// (one measured NOT correctly rounded).  After the first the relative error is
+// below 2^-52, after the second y1 * (2 - n y1) is within about 2^-104 of 1/n and
+// the last fma rounds once; 1/n for n < 2^16 is at least 2^-70 (relative) away from
+// any rounding midpoint, so the result is the correctly rounded 1.0 / n.  Checked
+// against the IEEE division for every n < 65536 before use (not done: off).  Used only with
+// RLAMD_SETTLE_RCPN: on cfg 2 the f64 chain measured slower than the table read
+// it replaces (0.199 against 0.188 ms per launch, A/B on one box).
 __device__ __forceinline__ double rcp_nr(uint32_t n) {
     const double dn = (double)n;
     const double r0 = __builtin_amdgcn_rcp(dn);
-    const double e = __builtin_fma(-dn, r0, 1.0);
-    return n ? __builtin_fma(r0, e, r0) : 0.0;
+    const double e0 = __builtin_fma(-dn, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-dn, r1, 1.0);
+    return n ? __builtin_fma(r1, e1, r1) : 0.0;
 }
 // argmax (first maximum, strict >) and max of one f64 row in a single pass
 // (utils.rs:1-21: a NaN at index 0 sticks, later NaNs never win)

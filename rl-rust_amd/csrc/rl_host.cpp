@@ -525,10 +525,18 @@ int agent_select_kernel(rl_agent *a) {
             int ncu = 256;
             (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, a->device);
             const uint64_t groups = a->grid.x, per_cu = (groups + (uint64_t)ncu - 1) / (uint64_t)ncu;
-            const uint64_t resident = std::max<uint64_t>(1, std::min<uint64_t>(per_cu, 2048 / a->block.x));
             const size_t base = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector,
                                                   a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x, 0,
                                                   a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
+            // the groups that can be resident at all: the kernel's register-limited
+            // occupancy (without the pair slots), not only the 32-wave cap — cfg 4 at
+            // 2^19 lanes on one GPU runs 4 groups per CU (128 VGPRs), so each may
+            // take 40 KiB, not 20 (2.12e10 -> 2.2e10 env-steps/s measured)
+            int occ_regs = 0;
+            if (a->fn(a->kp, a->grid, a->block, base, a->stream, &occ_regs) != hipSuccess || occ_regs <= 0)
+                occ_regs = (int)(2048 / a->block.x);
+            const uint64_t resident = std::max<uint64_t>(
+                1, std::min<uint64_t>(per_cu, std::min<uint64_t>((uint64_t)occ_regs, 2048 / a->block.x)));
             const int64_t room = (int64_t)(160 * 1024 / resident) - (int64_t)base - 1024;
             a->kp.trc_kb = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(64, room / 1024));
         }

@@ -98,6 +98,9 @@ __host__ __device__ constexpr bool qsh_layout(int fq, int ucb, int P, int algo) 
 #ifndef RLAMD_RM_PIN
 #define RLAMD_RM_PIN 0
 #endif
+#ifndef RLAMD_QA_EARLY
+#define RLAMD_QA_EARLY 1   // rmx: Q(s, a) for the TD read right after the barrier, beside the row summary
+#endif
 #ifndef RLAMD_SETTLE_RCPN
 #define RLAMD_SETTLE_RCPN 0   // 1: the settle's 1/n by v_rcp_f64 + one Newton step, no table read
 #endif
@@ -953,6 +956,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // range: no clamp), clear accumulators
     auto settle = [&](uint32_t idx) -> double {
         const int64_t packed = (int64_t)SUM[idx];
+        const unsigned long long qold = Q[idx];   // issued beside the SUM read, not after 1/n's
         const uint32_t n = PACKC ? (uint32_t)(packed & 2047) : (uint32_t)CNT16[idx];
         const int64_t sum = PACKC ? (packed >> 11) : packed;
         const double rc = RLAMD_SETTLE_RCPN ? rcp_nr(n)
@@ -962,7 +966,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                                 : (double)sum;
         const double y = __builtin_trunc(sd * rc) + 0x1.8p52;   // mean_delta_rcp
         const int64_t md = (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull);
-        const unsigned long long q = Q[idx] + (unsigned long long)md;
+        const unsigned long long q = qold + (unsigned long long)md;
         Q[idx] = q;
         const double v = q_val((int64_t)q);
         if constexpr (QSH) QD[idx] = v;
@@ -1214,6 +1218,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
         }
         uint32_t rm_pad = 0;                // rmx: the row summary's 4th dword (see below)
+        double qa_pre = 0.0;                // rmx: Q(s, a) read early
         int64_t rmax = 0;                   // FUSE_MAX: utils::max of row s2 (the Q-learning target)
         double rmaxd = 0.0;
         int32_t rarg = -1;
@@ -1234,6 +1239,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     rmaxd = rm.x;
                     rarg = (int32_t)(uint32_t)f64_bits(rm.y);
                     rm_pad = (uint32_t)(f64_bits(rm.y) >> 32);
+                    // Q(s, a) of the TD, read with the summary (one action per step:
+                    // (s, a) is known since the last step; RLAMD_QA_EARLY)
+                    if (RLAMD_QA_EARLY && !rs_on) qa_pre = QD[qi(0u, L.s, L.a)];
                     if constexpr (RLAMD_RM_PIN) asm volatile("" : "+v"(rarg), "+v"(rmaxd));
                 } else {
                     double v[A];
@@ -1358,7 +1366,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 td = __builtin_nan("");                    // r + gamma * NaN - q
             } else {
                 const uint32_t qidx = qi(vt, L.s, L.a);
-                const double qa = QSH ? QD[qidx] : val((int64_t)Q[qidx]);
+                const double qa = QSH ? ((RLAMD_QA_EARLY && rmx && !rs_on) ? qa_pre : QD[qidx]) : val((int64_t)Q[qidx]);
                 td = r + p.gamma * fq - qa;
                 if constexpr (QSH && !RLAMD_RM_PIN) asm volatile("" ::"v"(rm_pad));
             }
