@@ -461,12 +461,12 @@ __device__ __forceinline__ int64_t fq_raw(double d, int e) {
     return (int64_t)__builtin_rint(__builtin_ldexp(d, -e));
 }
 // 1.0 / n (0 for n == 0) without a table read: v_rcp_f64 and two Newton steps
-// (one measured NOT correctly rounded).  After the first the relative error is
-// below 2^-52, after the second y1 * (2 - n y1) is within about 2^-104 of 1/n and
-// the last fma rounds once; 1/n for n < 2^16 is at least 2^-70 (relative) away from
-// any rounding midpoint, so the result is the correctly rounded 1.0 / n.  Checked
-// against the IEEE division for every n < 65536 before use (not done: off).  Used only with
-// RLAMD_SETTLE_RCPN: on cfg 2 the f64 chain measured slower than the table read
+// (with one step the cfg 2 fixtures failed: not correctly rounded).  After the
+// first step the relative error is below 2^-52, after the second y1 * (2 - n y1)
+// is within about 2^-104 of 1/n and the last fma rounds once, and 1/n for small n
+// is far from any rounding midpoint, so this should be the correctly rounded
+// 1.0 / n — an argument, not a check: it is used only with RLAMD_SETTLE_RCPN,
+// which is off because on cfg 2 the f64 chain measured slower than the table read
 // it replaces (0.199 against 0.188 ms per launch, A/B on one box).
 __device__ __forceinline__ double rcp_nr(uint32_t n) {
     const double dn = (double)n;

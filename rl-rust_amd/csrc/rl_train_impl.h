@@ -101,6 +101,18 @@ __host__ __device__ constexpr bool qsh_layout(int fq, int ucb, int P, int algo) 
 #ifndef RLAMD_QA_EARLY
 #define RLAMD_QA_EARLY 1   // rmx: Q(s, a) for the TD read right after the barrier, beside the row summary
 #endif
+#ifndef RLAMD_RSUM_REG
+#define RLAMD_RSUM_REG 0   // 1: training-episode rewards summed per lane in registers, one LDS add per wave
+                           // at launch end (cfg 2: 0.1929 against 0.1896 ms per launch, A/B on one box)
+#endif
+#ifndef RLAMD_RUN_TRAIN
+#define RLAMD_RUN_TRAIN 0  // 1: throughput mode takes train == doS (a live lane is always in TRAIN mode);
+                           // with RSUM_REG 0.1903 ms, no gain
+#endif
+#ifndef RLAMD_QA_EARLY2
+#define RLAMD_QA_EARLY2 1   // traces (not UCB + expected SARSA): Q(s, a) read early (cfg 4: 0.5377 -> 0.5339 ms;
+                            // on cfg 5's one-step double tables it measured 0.3528 -> 0.3549: not used there)
+#endif
 #ifndef RLAMD_SETTLE_RCPN
 #define RLAMD_SETTLE_RCPN 0   // 1: the settle's 1/n by v_rcp_f64 + one Newton step, no table read
 #endif
@@ -1104,6 +1116,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     // wave-level per-launch counters (scalar registers: ballot popcounts)
     uint32_t c_train = 0, c_eval = 0, c_tep = 0, c_eep = 0;
     unsigned long long *const RSUM = &ACC[4];
+    // RLAMD_RSUM_REG: this lane's finished training episodes' rint(reward * 2^16),
+    // summed in registers (int64 adds are exact and order free)
+    int64_t rsum_lane = 0;
 
     // FrozenLake family, one action per step (no reset-and-step): the step's table
     // word trans[(s, a)] is read a step ahead (after the previous selection)
@@ -1217,6 +1232,15 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
             for (int i = 0; i < A; ++i) ra2[i] = rb2[i] = 0;
         }
+        // RLAMD_QA_EARLY2: the TD's Q(s, a) word (table vt) read with the target rows,
+        // its latency under the selection (L.s, L.a, L.dflag are final here, also
+        // after a fused reset)
+        int64_t qa_raw_pre = 0;
+        constexpr bool QAE2 = RLAMD_QA_EARLY2 && TRACES && !QSH && !SPEC;
+        if constexpr (QAE2) {
+            if (BJC && !bj_nonterminal(L.s)) qa_raw_pre = 0;   // never a TD source (terminal rows are not stepped from)
+            else qa_raw_pre = (int64_t)Q[qi((P == 2 && !L.dflag) ? 1u : 0u, L.s, L.a)];
+        }
         uint32_t rm_pad = 0;                // rmx: the row summary's 4th dword (see below)
         double qa_pre = 0.0;                // rmx: Q(s, a) read early
         int64_t rmax = 0;                   // FUSE_MAX: utils::max of row s2 (the Q-learning target)
@@ -1303,7 +1327,9 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         }
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
-        const bool train = doS && L.mode == RL_MODE_TRAIN;
+        // throughput mode (EPI 0): rl_agent_run leaves every live lane in TRAIN mode
+        // (no eval interleave, no target: after_step<0> never changes a mode)
+        const bool train = (EPI == 0 && RLAMD_RUN_TRAIN) ? doS : (doS && L.mode == RL_MODE_TRAIN);
         const uint32_t vt = (P == 2 && !L.dflag) ? 1u : 0u;   // get_values: flag ? alpha : beta
         const uint32_t ut = (P == 2 && L.dflag) ? 1u : 0u;    // update:     flag ? beta : alpha
         double td = 0.0;
@@ -1366,7 +1392,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 td = __builtin_nan("");                    // r + gamma * NaN - q
             } else {
                 const uint32_t qidx = qi(vt, L.s, L.a);
-                const double qa = QSH ? ((RLAMD_QA_EARLY && rmx && !rs_on) ? qa_pre : QD[qidx]) : val((int64_t)Q[qidx]);
+                const double qa = QSH ? ((RLAMD_QA_EARLY && rmx && !rs_on) ? qa_pre : QD[qidx])
+                                      : val(QAE2 ? qa_raw_pre : (int64_t)Q[qidx]);
                 td = r + p.gamma * fq - qa;
                 if constexpr (QSH && !RLAMD_RM_PIN) asm volatile("" ::"v"(rm_pad));
             }
@@ -1801,8 +1828,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             after_step<EPI>(p, L, s2, a2, r, term, tr, ev);
             // fixed point: the host also proved |episode reward| * 2^16 < 2^51
             // (delta_bound), so rint is the magic add
-            if (tr) atomicAdd(RSUM, (unsigned long long)(FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
-                                                             : rint_i64_small(L.epi_reward * 65536.0)));
+            if constexpr (RLAMD_RSUM_REG && !INSTR) {
+                const int64_t rq = FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0) : rint_i64_small(L.epi_reward * 65536.0);
+                rsum_lane += tr ? rq : (int64_t)0;
+            } else {
+                if (tr) atomicAdd(RSUM, (unsigned long long)(FQ ? (int64_t)__builtin_rint(L.epi_reward * 65536.0)
+                                                                 : rint_i64_small(L.epi_reward * 65536.0)));
+            }
             if (INSTR && p.elog && (tr || ev)) log_episode(p, lane, L, tr);
         } else if (doR) {
             L.s = s2;
@@ -1837,6 +1869,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         if constexpr (PAIRS) { if (active) pair_cache_store(p, pc, lane, tcnt); }
     }
     {
+        if constexpr (RLAMD_RSUM_REG && !INSTR) {
+            const int64_t rw = wave_sum_i64(rsum_lane);
+            if ((tid & 63u) == 0 && rw) atomicAdd(RSUM, (unsigned long long)rw);
+        }
         const uint32_t c_done = (uint32_t)__popcll(__ballot(active && L.mode == RL_MODE_DONE));
         if ((tid & 63u) == 0) {
             if (c_train) atomicAdd(&ACC[0], (unsigned long long)c_train);
