@@ -472,6 +472,8 @@ struct rl_agent {
 
 namespace {
 
+void agent_sync_params(rl_agent *a);
+
 int agent_select_kernel(rl_agent *a) {
     a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo,
                          a->priv ? 1 : 0);
@@ -533,6 +535,7 @@ int agent_select_kernel(rl_agent *a) {
             // 2^19 lanes on one GPU runs 4 groups per CU (128 VGPRs), so each may
             // take 40 KiB, not 20 (2.12e10 -> 2.2e10 env-steps/s measured)
             int occ_regs = 0;
+            agent_sync_params(a);   // the kernel the query names follows KParams::fq
             if (a->fn(a->kp, a->grid, a->block, base, a->stream, &occ_regs) != hipSuccess || occ_regs <= 0)
                 occ_regs = (int)(2048 / a->block.x);
             const uint64_t resident = std::max<uint64_t>(
