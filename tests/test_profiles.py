@@ -1,0 +1,37 @@
+"""CPU: the committed bench evidence (profiles/r04_bench/*.json) is internally
+consistent: every roofline fraction is a fraction (<= 1),
+counters are attached only from the benched build (rl_build_id equal), and the
+PMC summary they cite exists and holds that build's kernel time."""
+import glob
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04_bench", "*.json")))
+
+
+@pytest.mark.parametrize("path", LINES, ids=[os.path.basename(p) for p in LINES])
+def test_bench_line_roofline_is_consistent(path):
+    d = json.load(open(path))
+    r = d["roofline"]
+    assert 0.0 < r["frac"] <= 1.0, r["frac"]
+    assert r["bound"] in ("latency", "valu", "hbm")
+    assert r["hbm"]["fused_frac"] <= 1.0
+    if r["hbm"]["traffic_frac"] is not None:
+        assert r["hbm"]["traffic_frac"] <= 1.0
+    if r["counters"] is not None:
+        assert r["counters_build"].split()[0] == d["build_id"].split()[0]
+        summary = os.path.join(ROOT, r["counters"].split(":")[0])
+        assert os.path.exists(summary), summary
+        if r["bound"] in ("latency", "valu"):
+            assert r["frac"] == json.load(open(summary))["valu_pipe_frac"]
+    else:
+        assert r["bound"] == "hbm"
+
+
+def test_headline_line_is_the_default_workload():
+    d = json.load(open(os.path.join(ROOT, "profiles", "r04_bench", "bench_cfg2.json")))
+    assert d["config"]["survey_cfg"] == 2 and d["config"]["lanes_per_gpu"] == 1 << 20
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
