@@ -7,7 +7,9 @@ groups of 512 lanes (one workgroup, Q in LDS), merge every K=64 synchronous
 steps.  One bench "step" = one launch = K synchronous env-steps of every lane +
 the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
 §8(d): warm-up 64 synchronous steps (1 launch), timed window 4,096 (64 launches).
---config 3/4/5 selects the other §8(d) workloads (per-GPU lane counts).
+--config 3/4/5 selects the other §8(d) workloads (per-GPU lane counts); 6 and 7
+the §8(f) rows on private agents: frozen_lake_neural's NeuralPolicy and
+cliffwalking_model's Dyna-Q (InternalModelAgent, 10 planning steps).
 
   python bench.py [--gpus N --steps K --warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -47,7 +49,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
                     help="SURVEY §8(d) workload preset (2 = the headline)")
     ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU")
     ap.add_argument("--group", type=int, default=None, help="learner-group size (lanes per workgroup)")
@@ -67,8 +69,11 @@ def parse():
                     help="PMC summaries per workload (scripts/collect_counters.py)")
     a = ap.parse_args()
     for k, v in PRESETS[a.config].items():
-        if k != "reset_step" and getattr(a, k) is None:
+        if k not in ("reset_step", "extra") and getattr(a, k) is None:
             setattr(a, k, v)
+    a.extra = dict(PRESETS[a.config].get("extra", {}))
+    if "map8x8" in a.extra:
+        a.map8x8 = a.extra.pop("map8x8")
     if a.reset_step is None:
         a.reset_step = PRESETS[a.config].get("reset_step", 0)
     return a
@@ -87,6 +92,14 @@ PRESETS = {
             lanes=1 << 17, group=256, reset_step=1),
     5: dict(env="blackjack", agent="one_step", policy="double", selector="eps_greedy", algo="qlearning",
             lanes=1 << 19, group=512, reset_step=1),
+    # §8(f) rows, private agents (one agent per lane):
+    # src/bin/frozen_lake_neural.rs (FrozenLake 4x4, DenseLayer(1,32) -> leaky_relu6 ->
+    # DenseLayer(32,4), eps <- eps * 0.5) and src/bin/cliffwalking_model.rs (Dyna-Q)
+    6: dict(env="frozen_lake", agent="one_step", policy="neural", selector="eps_greedy", algo="qlearning",
+            lanes=1 << 20, group=1, extra=dict(map8x8=0, decay_kind=1, eps_decay=0.5, net_input="scalar",
+                                                net_hidden=32, net_act1="leaky_relu6", net_act2="linear")),
+    7: dict(env="cliff_walking", agent="one_step", policy="tabular", selector="eps_greedy", algo="qlearning",
+            lanes=1 << 20, group=1, extra=dict(planning=10)),
 }
 
 
@@ -137,7 +150,9 @@ def cpu_baseline(args):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     envk = {"frozen_lake": 0, "cliff_walking": 1, "taxi": 2, "blackjack": 3}[args.env]
     agentk = {"one_step": 0, "traces": 1}[args.agent]
-    polk = {"tabular": 0, "double": 1}[args.policy]
+    polk = {"tabular": 0, "double": 1, "neural": 2}[args.policy]
+    planning = args.extra.get("planning", 0)
+    map8 = args.map8x8
     selk = {"eps_greedy": 0, "ucb": 1}[args.selector]
     algok = {"sarsa": 0, "qlearning": 1, "expected_sarsa": 2}[args.algo]
     n, eval_at = 100000, 10000          # the bins: train(env, n_episodes, n_episodes / 10)
@@ -149,8 +164,8 @@ def cpu_baseline(args):
         return json.loads(out)
 
     def run_dense(reps, threads):
-        out = subprocess.run([dense, str(envk), str(args.map8x8), str(args.slippery), str(agentk), str(polk),
-                              str(selk), str(algok), str(n), str(eval_at), str(threads), str(reps)],
+        out = subprocess.run([dense, str(envk), str(map8), str(args.slippery), str(agentk), str(polk),
+                              str(selk), str(algok), str(n), str(eval_at), str(threads), str(reps), str(planning)],
                              check=True, capture_output=True, text=True).stdout
         return json.loads(out)
 
@@ -169,9 +184,23 @@ def cpu_baseline(args):
     # every core this process may run on (the box's share: sched_getaffinity, not
     # os.cpu_count(), which counts the whole machine)
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    desc = (f"{args.env}{' 8x8' if args.map8x8 and args.env == 'frozen_lake' else ''}"
-            f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} {args.algo} {args.selector}")
-    mine = (envk, args.map8x8, agentk, polk, selk, algok)
+    desc = (f"{args.env}{' 8x8' if map8 and args.env == 'frozen_lake' else ''}"
+            f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} {args.algo} {args.selector}"
+            f"{f' + Dyna {planning} planning steps' if planning else ''}")
+    mine = (envk, map8, agentk, polk, selk, algok)
+    if polk == 2 or planning:
+        # NeuralPolicy / InternalModelAgent: ref_faithful.c does not restate them, so
+        # the oracle's faithful loop (rlref.c rlo_faithful, bit-exact with the device
+        # in these rows, tests/test_gpu_parity.py) is the baseline
+        n = 10000 if polk == 2 else 2000
+        eval_at = n // 10
+        repd, d = sized(lambda k: run_dense(k, 1), args.cpu_seconds)
+        res = line("port", f"ref_dense (oracle/rlref.c rlo_faithful) {desc}", repd, d, 1)
+        reps_m, m = sized(lambda k: run_dense(k, threads), args.cpu_seconds / 2)
+        res["multi_core"] = line("port", f"{threads} independent rlo_faithful loops (len(os.sched_getaffinity(0)))",
+                                 reps_m, m, threads)
+        res["host_threads_machine"] = os.cpu_count()
+        return res
     reps, r = sized(lambda k: run_rf(*mine, k, 1), args.cpu_seconds)
     res = line("port", f"ref_faithful (oracle/ref_faithful.c: FxHashMap tables, ChaCha12, Vec histories) {desc}",
                reps, r, 1)
@@ -214,15 +243,29 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     rows = 484 if (args.env == "blackjack" and args.selector != "ucb") else agent.S   # LDS rows per group
     slot_bytes = 8 * agent.P * rows * agent.A * groups if agent.q_repr() == "f64" else 0
     fused_bytes = 2 * 56 * lanes + slot_bytes
+    if args.group == 1:
+        # private agents (one agent per lane, its tables / weights in HBM): per
+        # env-step the TD reads row s2 and Q(s, a) and writes Q(s, a) (tabular,
+        # + the same per Dyna planning step), or reads the weights for the two
+        # predicts and reads + writes them in the fit (NeuralPolicy)
+        if args.policy == "neural":
+            per_step = 4 * 8 * agent.net_dims()[2]
+        else:
+            per_step = 8 * (n_act + 2) * (1 + args.extra.get("planning", 0))
+        fused_bytes = 2 * 56 * lanes + per_step * steps_done / args.steps
     fused_frac = fused_bytes / avg_kern_s / HBM_PEAK
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     traffic_frac = (traffic / avg_kern_s / HBM_PEAK) if traffic else None
     pipe = pmc.get("valu_pipe_frac") if pmc else None
     wait = (pmc.get("wave_cycle_split") or {}).get("SQ_WAIT_ANY") if pmc else None
-    out = {"kernel": "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
+    out = {"kernel": "k_train_private" if args.group == 1 else "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
            "hbm": {"fused_bytes_per_launch": fused_bytes, "fused_frac": fused_frac,
-                   "fused_basis": "2 x 56 B lane record per lane per launch (+ 8 B x LDS entries per group "
-                                  "for f64 tables): the fused kernel keeps lanes in registers for K steps",
+                   "fused_basis": ("2 x 56 B lane record per lane per launch (+ 8 B x LDS entries per group "
+                                   "for f64 tables): the fused kernel keeps lanes in registers for K steps")
+                   if args.group != 1 else
+                   ("private agents: 2 x 56 B lane record per lane per launch + per env-step the lane's own "
+                    "table traffic (tabular: row s2, Q(s,a) read + written, x (1 + planning steps); neural: "
+                    "weights read by two predicts and read + written by the fit)"),
                    "traffic_bytes_per_launch": traffic, "traffic_frac": traffic_frac,
                    "peak_GBps": HBM_PEAK / 1e9},
            "hbm_priced": {"bytes_per_env_step": bytes_per_step, "GBps_equiv": priced / 1e9,
@@ -303,12 +346,15 @@ def main():
         dev = local_rank
     import rlamd
 
-    p = rlamd.default_params(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
-                             agent=args.agent, policy=args.policy, selector=args.selector,
-                             algo=args.algo, n_lanes=args.lanes, group_size=args.group,
-                             sync_every=args.sync, lane_offset=rank * args.lanes,
-                             device=dev)
+    kw = dict(env=args.env, map8x8=args.map8x8, slippery=args.slippery,
+              agent=args.agent, policy=args.policy, selector=args.selector,
+              algo=args.algo, n_lanes=args.lanes, group_size=args.group,
+              sync_every=args.sync, lane_offset=rank * args.lanes, device=dev)
+    kw.update({k: v for k, v in args.extra.items() if k != "planning"})
+    p = rlamd.default_params(**kw)
     agent = rlamd.Agent(p)
+    if args.extra.get("planning"):
+        agent.set_planning(args.extra["planning"])
     if args.reset_step:
         agent.set_reset_step(True)
     if args.q_mode != "auto":

@@ -698,8 +698,9 @@ static void *run_job(void *vp) {
     for (uint64_t k = 0; k < j->repeats; ++k) {
         history h = {{0, 0, 0, 8}, {0, 0, 0, 16}, {0, 0, 0, 8}, 0};
         j->train_steps += train(&ag, &e, j->n, j->eval_at, &h);
-        if (j->dump) {   /* Q of every dense state ([P][S][A], row or default), f64 bits, then histories */
-            for (int tb = 0; tb < (j->double_q ? 2 : 1); ++tb)
+        if (j->dump) {   /* dump 1: Q of every dense state ([P][S][A], row or default), f64 bits, then
+                            the histories' summary line; dump 2: the summary line only */
+            for (int tb = 0; tb < (j->dump == 1 ? (j->double_q ? 2 : 1) : 0); ++tb)
                 for (uint64_t s = 0; s < e.ns; ++s) {
                     double v[MAXA];
                     row_or_default(tb ? &ag.qb : &ag.qa, dense_to_id(j, s), v, e.A);
@@ -723,7 +724,7 @@ static void *run_job(void *vp) {
 
 int main(int argc, char **argv) {
     if (argc < 12) {
-        fprintf(stderr, "usage: %s env map8x8 slippery agent policy selector algo n_episodes eval_at repeats threads [dump]\n",
+        fprintf(stderr, "usage: %s env map8x8 slippery agent policy selector algo n_episodes eval_at repeats threads [dump 0|1|2]\n",
                 argv[0]);
         return 2;
     }

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("round")
     ap.add_argument("--config", type=int, required=True)
     ap.add_argument("--slippery", type=int, default=0)
-    ap.add_argument("--kernel", default="k_train_shared")
+    ap.add_argument("--kernel", default=None, help="default: k_train_private for group 1 presets, else k_train_shared")
     ap.add_argument("--q-mode", default="auto")
     ap.add_argument("--lanes", type=int, default=None)
     a = ap.parse_args()
@@ -44,7 +44,7 @@ def main():
             build_id = json.loads(line).get("build_id")
     if not build_id:
         sys.exit(f"no bench line with a build_id in {a.profdir}/trace.log")
-    s = summarize(a.profdir, a.kernel)
+    s = summarize(a.profdir, a.kernel or ("k_train_private" if pr["group"] == 1 else "k_train_shared"))
     prof = os.path.join(ROOT, "profiles")
     stem = f"{a.round}_{key}"
     shutil.copy(os.path.join(a.profdir, "trace", "run_kernel_stats.csv"),

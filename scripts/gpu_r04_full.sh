@@ -16,7 +16,7 @@ run() {   # key, bench args
 import json; d=json.load(open('gpurun_out/bench_$1.json')); r=d['roofline']
 print('$1', '%.4g'%d['value'], 'kern_ms %.4f'%r['kernel_avg_ms'], r['bound'], 'frac %.3f'%r['frac'], 'cpu', d.get('cpu_baseline',{}).get('value'))"
 }
-for k in ${BENCH:-cfg2 cfg2_slippery cfg2_f64 cfg3 cfg4 cfg4_2p19 cfg5}; do
+for k in ${BENCH:-cfg2 cfg2_slippery cfg2_f64 cfg3 cfg4 cfg4_2p19 cfg5 cfg6 cfg7}; do
   case $k in
     cfg2) run cfg2 "" ;;
     cfg2_slippery) run cfg2_slippery "--config 2 --slippery 1 $CPU" ;;
@@ -25,5 +25,7 @@ for k in ${BENCH:-cfg2 cfg2_slippery cfg2_f64 cfg3 cfg4 cfg4_2p19 cfg5}; do
     cfg4) run cfg4 "--config 4 $CPU" ;;
     cfg4_2p19) run cfg4_2p19 "--config 4 --lanes 524288 --no-cpu-baseline" ;;
     cfg5) run cfg5 "--config 5 $CPU" ;;
+    cfg6) run cfg6 "--config 6 $CPU" ;;
+    cfg7) run cfg7 "--config 7 $CPU" ;;
   esac
 done

@@ -13,6 +13,8 @@ for spec in ${PROF:-cfg2 cfg2_slippery cfg3 cfg4 cfg5}; do
     cfg4) a="--config 4" ;;
     cfg4_2p19) a="--config 4 --lanes 524288" ;;
     cfg5) a="--config 5" ;;
+    cfg6) a="--config 6" ;;
+    cfg7) a="--config 7" ;;
   esac
   ROUND=r04_$spec BENCH_ARGS="$a" bash scripts/profile.sh > gpurun_out/profile_$spec.log 2>&1 || { rc=$?; echo "profile $spec rc=$rc"; tail -5 gpurun_out/profile_$spec.log; exit $rc; }
   echo "profiled $spec"
