@@ -49,11 +49,13 @@ def main():
     stem = f"{a.round}_{key}"
     shutil.copy(os.path.join(a.profdir, "trace", "run_kernel_stats.csv"),
                 os.path.join(prof, stem + "_kernel_stats.csv"))
-    try:
-        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
-                              text=True).stdout.strip()
-    except OSError:
-        head = "?"
+    head = os.environ.get("RLAMD_HEAD")   # set by the GPU-box scripts (no .git there)
+    if not head:
+        try:
+            head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                  text=True).stdout.strip()
+        except OSError:
+            head = "?"
     s["dir"] = f"{a.profdir} (copied; build at HEAD {head or '?'})"
     json.dump(s, open(os.path.join(prof, stem + "_summary.json"), "w"), indent=1)
     path = os.path.join(prof, "counters.json")
