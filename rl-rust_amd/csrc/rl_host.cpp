@@ -448,7 +448,6 @@ struct rl_agent {
     rl_step_record *rec_d = nullptr;
     bool recording = false;
     std::vector<rl_step_record> rec_h;
-    unsigned long long *dbg_d = nullptr;   // -DRLAMD_STAMPS builds: the step loop's segment cycles
     rl_episode_record *elog_d = nullptr;   // episode log ring [cap][L]
     uint32_t *elog_cnt_d = nullptr;
     uint32_t elog_cap = 0;
@@ -1394,11 +1393,6 @@ int rl_agent_create(const rl_agent_config *cfg, rl_agent **out) {
     p.target_episodes = 0; p.eval_at = 0; p.eval_div = 0; p.eval_episodes = c.eval_episodes; p.eval_only = 0;
     p.stats = a->stats_d;
     p.rec = nullptr;
-#if RLAMD_STAMPS
-    if ((rc = dalloc(&a->dbg_d, 64))) return bad(rc);
-    HIPC(hipMemset(a->dbg_d, 0, 64 * sizeof(unsigned long long)));
-#endif
-    p.dbg = a->dbg_d;
     agent_sync_params(a);
     if ((rc = agent_select_kernel(a))) return bad(rc);
     launch_lane_init(c.env.kind, p, c.seed, c.lane_offset, c.eps0, a->stream);
@@ -1419,17 +1413,6 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->delta_rep);
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
-#if RLAMD_STAMPS
-    if (a->dbg_d) {   // diagnostic build: the segment sums on stderr
-        unsigned long long h[64] = {0};
-        if (hipMemcpy(h, a->dbg_d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
-            fprintf(stderr, "rlamd_stamps:");
-            for (int i = 0; i < 64; ++i) fprintf(stderr, " %llu", h[i]);
-            fprintf(stderr, "\n");
-        }
-    }
-    dfree(a->dbg_d);
-#endif
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
     dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d); dfree(a->call_d);

@@ -156,9 +156,6 @@ struct KParams {
     // the other wave slots idle
     uint32_t lpw;
     uint32_t trc_kb;       // LDS KiB per learner group for pair-trace slots (rl_train_impl.h smem_layout)
-    // diagnostic builds only (-DRLAMD_STAMPS=1): per-segment wave cycles of the
-    // shared kernels' step loop, u64[64]; null otherwise
-    unsigned long long *dbg;
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

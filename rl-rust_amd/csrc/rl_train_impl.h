@@ -426,22 +426,6 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
-#ifndef RLAMD_STAMPS
-#define RLAMD_STAMPS 0   // diagnostic builds: wave cycles per step-loop segment into KParams::dbg
-#endif
-constexpr int RLAMD_NSEG = 11;
-// s_memtime with its wait in one statement, fenced from the scheduler
-// (cdna_hip_programming.md §7 "In-kernel stamps"): diagnostic builds only
-__device__ __forceinline__ uint64_t stamp_now() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#ifndef RLAMD_SPIN_SLEEP
-#define RLAMD_SPIN_SLEEP 1   // UCB + expected SARSA: s_sleep between polls of the step's arrival count
-#endif
 #ifndef RLAMD_BJ_ONE_LOOP
 // Blackjack learner groups: reset and step draws in one loop (EnvDev::advance).
 // Parity-green but measured slower on cfg 5 (4.98e10 vs 5.83e10 env-steps/s on
@@ -1144,19 +1128,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, L.s, L.a)];
     // reset-and-step in effect (uniform over the block)
     const bool rs_on = (!UCB && RS != 0) && (RS == 1 || p.reset_step);
-    // RLAMD_STAMPS: segment sums (0 env step, 1 the settle barrier, 2 flags / rows /
-    // selection, 3 UCB counters, 4 TD, 5-6 contributions and their barriers, 7 settle,
-    // 8 counter fold + end barrier, 9 bookkeeping; 10 iterations), wave-uniform points
-    uint64_t st_acc[RLAMD_NSEG] = {};
-    uint64_t st_prev = 0;
-    auto stamp = [&](int i) {
-        if constexpr (RLAMD_STAMPS) {
-            const uint64_t t = stamp_now();
-            st_acc[i] += t - st_prev;
-            st_prev = t;
-        }
-    };
-    if constexpr (RLAMD_STAMPS) st_prev = stamp_now();
     for (uint32_t k = 0; k < p.K; ++k) {
         // ---------------- one synchronous step: each live lane either RESETs
         // (env.reset() + get_action, src/agent.rs:83-84) or STEPs (env.step +
@@ -1226,12 +1197,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
-        stamp(0);
         // the previous step's settle (Q, flags, counters) before this step's reads:
         // the env step above touches no shared table, so it overlaps the settle
         // (reset-and-step reads Q for its reset lanes' selection: barrier at the end of the step)
         if (RLAMD_LATE_B3 && k > 0 && !rs_on) __syncthreads();
-        stamp(1);
         // UCB + expected SARSA (SPEC): the visible flags of row s2 decide most of
         // the step without Q values or counters (the regime is mostly
         // non-finite rows).  u_0 NaN sticks as the argmax (utils.rs:1-11); any
@@ -1315,7 +1284,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         // the next step's table word (s2, a2) read now: the table is constant, and
         // the read's latency then overlaps the update and its barriers
         if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, s2, a2)];
-        stamp(2);
         uint32_t d_own = 0xffffffffu;   // SPEC: the step-count entry this lane folds at step end
         if constexpr (SPEC) {
             // the step's increments go to the step counts / T[1], apart from what this
@@ -1346,7 +1314,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 const uint32_t goal = (k + 1u) * (nthr >> 6);
                 while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ARR, __ATOMIC_RELAXED,
                                                                         __HIP_MEMORY_SCOPE_WORKGROUP)) < goal)
-                    __builtin_amdgcn_s_sleep(RLAMD_SPIN_SLEEP);
+                    __builtin_amdgcn_s_sleep(1);
                 __threadfence_block();
             }
             lnt_ok = false;   // this step's probabilities and the next selection use ln(T_{k+1})
@@ -1357,7 +1325,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if ((tid & 63u) == 0 && c) atomicAdd(&T[0], (unsigned long long)c);
             // the next reader is the next step's selection, after the end-of-step barrier
         }
-        stamp(3);
         // ---------------- update (one_step_agent.rs:53-86 / elegibility_traces_agent.rs:61-104)
         // Contributions go to SUM/CNT, never to Q, so no barrier is needed before them.
         // throughput mode (EPI 0): rl_agent_run leaves every live lane in TRAIN mode
@@ -1431,7 +1398,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if constexpr (QSH && !RLAMD_RM_PIN) asm volatile("" ::"v"(rm_pad));
             }
         }
-        stamp(4);
         if constexpr (!TRACES) {
             const uint32_t idx = qi(ut, L.s, L.a);
             if constexpr (FQ) {
@@ -1449,7 +1415,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     owner = old == 0u;
                 }
                 __syncthreads();   // every code in
-                stamp(5);
                 // pass 2: the contribution on its entry's grid, and the count — only
                 // where every contribution was finite: an entry with non-finite kinds
                 // moves by their IEEE sum, which needs neither (settle_fq)
@@ -1463,14 +1428,12 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     if (!RLAMD_NF_SKIP) atomicAdd(&W[idx], 1u);
                 }
                 __syncthreads();   // all contributions in, all Q reads done
-            stamp(6);
                 if (sweep) { if (tid < PSAL) settle_fq(tid); }
                 else if (owner) settle_fq(idx);
             } else {
                 bool owner = false;
                 if (train) owner = contribute(idx, rint_i64_small(p.lr40 * td), 1u);   // q_fix_inrange(lr * td)
                 __syncthreads();   // all contributions in, all Q reads done
-            stamp(6);
                 if (rmx) {
                     if constexpr (RLAMD_SETTLE_QUAD) { if (tid < PSAL) settle_quad(tid); }
                     else { if (tid < PSAL / 2u) settle_pair(tid); }
@@ -1491,7 +1454,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 __syncthreads();
                 e_tr = fq_grid(GCODE[0]) + p.trace_k;
             }
-            stamp(5);
             // a visited state's row count n += 1 (settle_row's mean)
             auto row_hit = [&](uint32_t rid) {
                 if (rsweep) atomicAdd(&CNTR[rid], 1u);
@@ -1801,7 +1763,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             }
             if (train && term) tcnt = 0;                  // the trace map is cleared
             __syncthreads();   // all contributions in, all Q reads done
-            stamp(6);
             if (tid == 0) GCODE[0] = 0u;                  // read by every thread before the sweep
             if (rsweep) {
                 for (uint32_t r = tid; r < (uint32_t)P * SL; r += nthr) settle_row(r, e_tr);
@@ -1812,7 +1773,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 if (tid == 0) LISTN[0] = 0u;
             }
         }
-        stamp(7);
         if constexpr (SPEC) {                     // fold the step's counter increments
             if (d_own != 0xffffffffu) {
                 if (p.ucb_pack) {
@@ -1829,7 +1789,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         // the next step's env step instead, below; reset-and-step reads Q first —
         // and a barrier between its deal and its reads measured 0.98x on cfg 5)
         if (!RLAMD_LATE_B3 || rs_on) __syncthreads();
-        stamp(8);
         bool tr = false, ev = false;
         if constexpr (!INSTR && RLAMD_TAIL) {
             // one predicated block (no STEP / RESET branches): the STEP lanes'
@@ -1895,8 +1854,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 c_eep += (uint32_t)__popcll(__ballot(ev));
             }
         }
-        stamp(9);
-        if constexpr (RLAMD_STAMPS) st_acc[10] += 1;
     }
 
     if (active) lane_store(p, lane, L);
@@ -1929,10 +1886,6 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             if ((tid & 63u) == 0 && ts) atomicAdd(&ACC[7], (unsigned long long)ts);
         }
         flush_block(p, ACC);
-        if constexpr (RLAMD_STAMPS) {
-            if ((tid & 63u) == 0 && p.dbg)
-                for (int i = 0; i < RLAMD_NSEG; ++i) atomicAdd(&p.dbg[i], (unsigned long long)st_acc[i]);
-        }
     }
 
     // ---------------- emit this group's changes for the merge.  Fixed point:
