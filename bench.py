@@ -227,7 +227,9 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     than 40 % of their cycles while the pipe is below 70 %,
     "valu" when the pipe is the closer ceiling, else "hbm".  The HBM side is
     reported as measured traffic (PMC) and as the fused kernel's algorithmic bytes
-    (every lane record read and written once per launch), both <= 1 of the peak.
+    (every lane record read and written once per launch), both <= 1 of the peak;
+    when the measured traffic is the nearer ceiling (the private agents' own tables
+    and weights in HBM) `frac` is the HBM fraction (`ceiling`: "hbm").
     SURVEY §8(d)'s 32 B/env-step price assumes a lane-record round trip per step,
     which the fused kernel does not make; it is kept under `hbm_priced` as a ratio,
     not a fraction."""
@@ -276,20 +278,21 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
            "counters": pmc.get("source") if pmc else None,
            "counters_build": pmc.get("build_id") if pmc else None}
     if pipe is not None:
-        if wait is not None and wait > 0.4 and pipe < 0.7:
-            bound = "latency"
-        elif traffic_frac is None or pipe >= traffic_frac:
-            bound = "valu"
+        # the ceiling: whichever of the VALU pipe and HBM the kernel runs closer to
+        ceiling = "hbm" if traffic_frac is not None and traffic_frac > pipe else "valu"
+        top = traffic_frac if ceiling == "hbm" else pipe
+        bound = "latency" if (wait is not None and wait > 0.4 and top < 0.7) else ceiling
+        basis = ("'latency': SQ_WAIT_ANY > 0.4 of wave cycles with both the VALU pipe and HBM below 0.7 of "
+                 "their peaks; frac is the nearer ceiling's (`ceiling`)")
+        if ceiling == "hbm":
+            out.update(bound=bound, ceiling="hbm", achieved=traffic / avg_kern_s / 1e9, peak=HBM_PEAK / 1e9,
+                       unit="GB/s", frac=traffic_frac, traffic=traffic, wait_frac=wait, valu_pipe_frac=pipe,
+                       basis="measured HBM bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE) / kernel time; " + basis)
         else:
-            bound = "hbm"
-        if bound == "hbm":
-            out.update(bound="hbm", achieved=traffic / avg_kern_s / 1e9, peak=HBM_PEAK / 1e9, unit="GB/s",
-                       frac=traffic_frac, traffic=traffic)
-        else:
-            out.update(bound=bound, achieved=pipe, peak=1.0, unit="VALU pipe occupancy (gfx950 model)",
+            out.update(bound=bound, ceiling="valu", achieved=pipe, peak=1.0, unit="VALU pipe occupancy (gfx950 model)",
                        frac=pipe, traffic=traffic, wait_frac=wait,
                        basis="(2 x SQ_INSTS_VALU + 2 x (f64 add/mul/fma + int64) + 6 x f64 trans) cycles / "
-                             "(cycles x 1024 SIMDs); 'latency': SQ_WAIT_ANY > 0.4 of wave cycles with the pipe < 0.7")
+                             "(cycles x 1024 SIMDs); " + basis)
     else:
         out.update(bound="hbm", achieved=fused_bytes / avg_kern_s / 1e9, peak=HBM_PEAK / 1e9, unit="GB/s",
                    frac=fused_frac, traffic=None,

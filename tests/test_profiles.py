@@ -25,8 +25,12 @@ def test_bench_line_roofline_is_consistent(path):
         assert r["counters_build"].split()[0] == d["build_id"].split()[0]
         summary = os.path.join(ROOT, r["counters"].split(":")[0])
         assert os.path.exists(summary), summary
-        if r["bound"] in ("latency", "valu"):
-            assert r["frac"] == json.load(open(summary))["valu_pipe_frac"]
+        sm = json.load(open(summary))
+        if r.get("ceiling", "valu" if r["bound"] in ("latency", "valu") else "hbm") == "valu":
+            assert r["frac"] == sm["valu_pipe_frac"]
+        else:
+            assert r["frac"] == r["hbm"]["traffic_frac"]
+            assert r["traffic"] == sm["hbm_bytes_per_launch"]["total"]
     else:
         assert r["bound"] == "hbm"
 
