@@ -426,6 +426,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_LAZY_ROWS
+#define RLAMD_LAZY_ROWS 1   // reset-and-step: the reset's selection reads its row only for exploiting lanes
+#endif
 #ifndef RLAMD_BJ_ONE_LOOP
 // Blackjack learner groups: reset and step draws in one loop (EnvDev::advance).
 // Parity-green but measured slower on cfg 5 (4.98e10 vs 5.83e10 env-steps/s on
@@ -944,6 +947,24 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             return argmax<A>(u);
         }
     };
+    // the fused reset's selection (RLAMD_LAZY_ROWS, eps-greedy without FUSE_MAX): row
+    // s is read only by the lanes that exploit — the draws come first either way, so
+    // the stream and the result are select()'s
+    auto select_lazy = [&](uint32_t s) -> uint32_t {
+        bool explore = L.eps != 0.0;
+        if (explore) explore = eps_test(L.rng, L.eps);
+        if (explore) return uniform_action<A>(L.rng);
+        int64_t ra[A], rb[A];
+        load_rows(s, ra, rb);
+        if constexpr (FQ) {
+            double v[A];
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = P == 2 ? (as_f64(ra[i]) + as_f64(rb[i])) / 2.0 : as_f64(ra[i]);
+            return argmax<A>(v);
+        } else {
+            return argmax_i64<A>(ra);
+        }
+    };
     // fixed point: add n contributions summing to `sum` to entry idx.  Sweep form
     // (the table fits the block, PSA <= nthr): thread i settles entry i every step,
     // so the counter add needs no return value.  Owner form: the step's first
@@ -1146,7 +1167,16 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         bool fused = false;
         if constexpr (!UCB && RS != 0) {   // RS: the schedule as a compile-time constant (-1: KParams)
             if (RS == 1 || p.reset_step) {
-                if (doR) {
+                if (doR && RLAMD_LAZY_ROWS && !FUSE_MAX) {
+                    const uint32_t s0 = E::reset(L.z, L.rng, tabs);
+                    L.ready = true;
+                    L.a = select_lazy(s0);
+                    L.s = s0;
+                    L.need_reset = false;
+                    L.epi_reward = 0.0;
+                    L.epi_len = 0;
+                    fused = true;
+                } else if (doR) {
                     const uint32_t s0 = E::reset(L.z, L.rng, tabs);
                     L.ready = true;
                     load_rows(s0, ra2, rb2);
