@@ -27,10 +27,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
-LAUNCHES = {"cfg2": 65, "cfg2_slippery": 65, "cfg3": 65, "cfg4": 65, "cfg5": 65}
+LAUNCHES = {"cfg2": 65, "cfg2_slippery": 65, "cfg3": 65, "cfg4": 65, "cfg5": 65, "cfg4_2p19": 65}
 # name -> (SURVEY cfg, extra bench.py arguments); cfg 2 is the headline (the
 # proven fixed point, k_train_shared_o8: VERDICT r03 item 3)
-CASES = {"cfg2": (2, {}), "cfg2_slippery": (2, {"slippery": 1}), "cfg3": (3, {}), "cfg4": (4, {}), "cfg5": (5, {})}
+CASES = {"cfg2": (2, {}), "cfg2_slippery": (2, {"slippery": 1}), "cfg3": (3, {}), "cfg4": (4, {}), "cfg5": (5, {}),
+         # BASELINE's whole cfg 4 (2^19 lanes) on one GPU, as bench.py --config 4 --lanes 524288
+         "cfg4_2p19": (4, {"n_lanes": 1 << 19})}
 
 
 def b64(a):
@@ -54,23 +56,36 @@ def run(name, mode):
     return kw, b
 
 
+def _arrays(args):
+    """one oracle run's results as plain arrays (picklable: the two modes of a case
+    run in parallel processes)"""
+    name, mode = args
+    kw, b = run(name, mode)
+    out = {"kw": kw, "q": b.q(), "q_raw": b.q_raw(), "q_repr": b.q_repr(), "stats": b.stats()[:10],
+           "eps": b.lane_eps()}
+    if kw.get("selector") == "ucb":
+        out["ucb"] = b.ucb()
+    return out
+
+
 def case(name):
-    kw, b = run(name, "auto")
-    q = b.q()
+    with ProcessPoolExecutor(max_workers=2) as ex:
+        a, sq = ex.map(_arrays, [(name, "auto"), (name, "f64_seq")])
+    kw = a["kw"]
+    q = a["q"]
     fin = np.isfinite(q)
-    out = {"survey_cfg": CASES[name][0], "params": kw, "launches": LAUNCHES[name], "q_repr": b.q_repr(),
-           "q_raw_i64_b64": b64(b.q_raw().astype("<i8")),
+    out = {"survey_cfg": CASES[name][0], "params": kw, "launches": LAUNCHES[name], "q_repr": a["q_repr"],
+           "q_raw_i64_b64": b64(a["q_raw"].astype("<i8")),
            "n_nan": int(np.isnan(q).sum()), "n_inf": int(np.isinf(q).sum()),
            "max_abs_finite": float(np.abs(q[fin]).max()) if fin.any() else 0.0,
-           "stats_u64": [int(x) for x in b.stats()[:10]],
-           "eps_sha256": sha(b.lane_eps().astype("<f8"))}
-    if kw.get("selector") == "ucb":
-        n, t = b.ucb()
+           "stats_u64": [int(x) for x in a["stats"]],
+           "eps_sha256": sha(a["eps"].astype("<f8"))}
+    if "ucb" in a:
+        n, t = a["ucb"]
         out["ucb_n_u64_b64"] = b64(np.asarray(n, "<u8"))
         out["ucb_t"] = int(t)
     # drift measurement: sequential f64 sums (same draws, same mean rule)
-    _, s = run(name, "f64_seq")
-    qs = s.q()
+    qs = sq["q"]
     both = np.isfinite(q) & np.isfinite(qs)
     d = np.abs(q[both] - qs[both])
     out["seq_sum_drift"] = {

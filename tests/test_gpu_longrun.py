@@ -1,7 +1,8 @@
 """GPU parity over the whole benchmarked window.
 
 bench.py's cfg 2 / 2-slippery / 3 / 4 / 5 presets (2^20 / 2^20 / 2^20 / 2^17 /
-2^19 lanes per GPU, groups of 512 / 512 / 512 / 256 / 512, K = 64) run for the
+2^19 lanes per GPU, groups of 512 / 512 / 512 / 256 / 512, K = 64), and cfg 4 at
+BASELINE's whole 2^19 lanes on one GPU (`bench.py --config 4 --lanes 524288`), run for the
 65 launches one default bench run makes (1 warm-up + 64 timed) and are compared
 with `tests/golden/longrun.json`, made by the oracle's batched schedule in the
 representation each configuration gets: the proven 2^-40 fixed point for the
@@ -32,7 +33,7 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5", "cfg4_2p19"])
 def test_bench_window_matches_oracle(rl, name):
     sys.path.insert(0, HERE)
     from golden.make_fullsize import bench_params
