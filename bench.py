@@ -30,6 +30,7 @@ by rl_build_id), see roofline(); `cpu_baseline` times C restatements of the
 reference loop on the host cores (bounded samples).
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -51,7 +52,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
                     help="SURVEY §8(d) workload preset (2 = the headline)")
-    ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU")
+    ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU (weak scaling: per-GPU work fixed)")
+    ap.add_argument("--lanes-total", type=int, default=None,
+                    help="env lanes over all GPUs (strong scaling: lanes per GPU = total / N); the north "
+                         "star's '2^20 parallel envs at 8xMI355X' is --lanes-total 1048576 --gpus 8")
     ap.add_argument("--group", type=int, default=None, help="learner-group size (lanes per workgroup)")
     ap.add_argument("--sync", type=int, default=64, help="K: synchronous steps per launch")
     for k in ("env", "agent", "policy", "selector", "algo"):
@@ -66,8 +70,9 @@ def parse():
     # HIP events around EVERY launch cost 3 % of the headline's throughput (measured in
     # the driver's shape, --steps 20 --warmup 5: 3.19e11 with, 3.30e11 without; events
     # on every 4th launch 3.26e11): the kernel's average duration is sampled instead
-    ap.add_argument("--timing-every", type=int, default=8,
-                    help="HIP events around every N-th timed launch (the kernel's average duration; 0: none)")
+    ap.add_argument("--timing-every", type=int, default=None,
+                    help="HIP events around every N-th timed launch (the kernel's average duration; 0: none); "
+                         "default 8, 1 for the private rows (a 100-ms launch hides the events' cost)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--counters-file", default=os.path.join(ROOT, "profiles", "counters.json"),
@@ -81,6 +86,8 @@ def parse():
         a.map8x8 = a.extra.pop("map8x8")
     if a.reset_step is None:
         a.reset_step = PRESETS[a.config].get("reset_step", 0)
+    if a.timing_every is None:
+        a.timing_every = 1 if a.group == 1 else 8
     return a
 
 
@@ -112,6 +119,28 @@ def workload_key(args):
     return (f"cfg{args.config}" + ("_slippery" if args.slippery else "") +
             (f"_{args.q_mode}" if args.q_mode != "auto" else "") + (f"_L{args.lanes}" if args.lanes != PRESETS[
                 args.config]["lanes"] else ""))
+
+
+GLOBAL_Q = os.path.join(ROOT, "tests", "golden", "global_q.json")
+
+
+def q_fixture(args, world):
+    """The oracle's one-process result for this run's GLOBAL lane set, if committed
+    (tests/golden/global_q.json, tests/golden/make_global_q.py): integer merges make
+    Q identical for any rank count at a fixed global lane set, so the
+    SHA-256 of the merged raw Q words is a known answer for an N-rank run."""
+    try:
+        tab = json.load(open(GLOBAL_Q))["cases"]
+    except (OSError, ValueError, KeyError):
+        return None
+    want = {"env": args.env, "agent": args.agent, "policy": args.policy, "selector": args.selector,
+            "algo": args.algo, "map8x8": args.map8x8, "slippery": args.slippery, "reset_step": int(args.reset_step),
+            "q_mode": args.q_mode, "global_lanes": world * args.lanes, "group": args.group, "sync": args.sync,
+            "launches": args.warmup + args.steps}
+    for name, c in tab.items():
+        if all(c["key"].get(k) == v for k, v in want.items()):
+            return name, c
+    return None
 
 
 def counters_for(args, build_id):
@@ -338,6 +367,13 @@ def main():
     dist_on = world > 1 or os.environ.get("RLAMD_FORCE_COMM") == "1"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    scaling = "weak"
+    if args.lanes_total is not None:     # strong scaling: the global lane set is fixed
+        if args.lanes_total % world or (args.lanes_total // world) % args.group:
+            raise SystemExit(f"--lanes-total {args.lanes_total}: not {world} equal shards of whole "
+                             f"learner groups of {args.group}")
+        args.lanes = args.lanes_total // world
+        scaling = "strong"
     # collective "rccl" (default): librlamd's own RCCL all-reduce in every merge,
     # and its communicator also runs the barriers and the max-over-ranks time —
     # no PyTorch anywhere.  "torch": a torch.distributed all_reduce of the merge
@@ -430,29 +466,60 @@ def main():
         total_steps = steps_done
     value = total_steps / wall
     avg_kern_s = kern_ms / n_kern / 1e3 if n_kern else wall / args.steps
+    # the merged Q after the run (untimed): SHA-256 of its raw int64 words, every
+    # rank's digest compared, and the committed one-process answer for this global
+    # lane set when there is one (a self-checking N-rank run)
+    q_check = None
+    if args.group != 1:
+        qh = hashlib.sha256(agent.q_raw().astype("<i8").tobytes()).hexdigest()
+        agree = True
+        if comm is not None:              # 48 bits of the digest are exact in an f64
+            h48 = float(int(qh[:12], 16))
+            agree = bool(comm.allreduce([h48], "max")[0] == comm.allreduce([h48], "min")[0])
+        elif dist is not None:
+            t = torch.tensor([int(qh[:12], 16)], dtype=torch.int64)
+            t2 = t.clone()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t2, op=dist.ReduceOp.MIN)
+            agree = bool(t.item() == t2.item())
+        fx = q_fixture(args, world)
+        st_all = st1["train_steps"]
+        if comm is not None:
+            st_all = int(comm.allreduce([float(st_all)], "sum")[0])
+        elif dist is not None:
+            ts = torch.tensor([st_all], dtype=torch.int64)
+            dist.all_reduce(ts)
+            st_all = int(ts.item())
+        q_check = {"q_sha256": qh, "ranks_agree": agree, "launches": args.warmup + args.steps,
+                   "global_lanes": world * args.lanes, "train_steps_all_ranks": st_all,
+                   "fixture": fx[0] if fx else None,
+                   "match": (fx[1]["q_sha256"] == qh and fx[1]["train_steps"] == st_all) if fx else None}
     bid = rlamd.build_id()
     pmc = counters_for(args, bid)
     q_repr = agent.q_repr()
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": ("f64 TD arithmetic; shared Q int64 fixed point 2^-40 (range proven, |Q| <= 2048, no clamp)"
                   if q_repr == "fixed40" else f"f64 TD arithmetic; shared Q f64 ({q_repr}: the reference's full range)"),
         "data": "synthetic (env lanes seeded per global lane id; no dataset)",
         "config": {"workload": f"run mode (rl_agent_run: lanes train continuously, eval interleave off) "
                                f"{args.env}{(' 8x8' if args.map8x8 else ' 4x4') if args.env == 'frozen_lake' else ''}"
                                f"{' slippery' if args.slippery else ''} {args.agent} {args.policy} "
-                               f"{args.algo} {args.selector}, {args.lanes} lanes/GPU",
+                               f"{args.algo} {args.selector}, {args.lanes} lanes/GPU"
+                               f"{f' ({world * args.lanes} in total, fixed)' if scaling == 'strong' else ''}",
                    "survey_cfg": args.config,
                    "schedule": "reset-and-step" if args.reset_step else "one action per synchronous step",
-                   "lanes_per_gpu": args.lanes, "group_size": args.group, "sync_every": args.sync,
+                   "lanes_per_gpu": args.lanes, "lanes_total": world * args.lanes,
+                   "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
                    "collective": ("rccl int64 all-reduces of the merge buffer (librlamd)" if collective == "rccl"
                                   else "torch all_reduce (rehearsal)") if dist_on else "none",
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"],
                    "q_repr": q_repr, "q_mode": args.q_mode},
+        "q_check": q_check,
         "build": rlamd.lib().rl_build_info().decode(),
         "build_id": bid,
         "roofline": roofline(args, agent, steps_done, avg_kern_s, pmc),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 5
+#define RL_ABI_VERSION 6
 
 enum rl_status {
     RL_OK = 0,
@@ -283,10 +283,13 @@ int rl_agent_get_action(rl_agent *a, uint32_t lane, uint64_t obs, uint32_t *acti
  * internal_model_agent.rs:47-77 when planning is on): *td = the TD error it returns */
 int rl_agent_update(rl_agent *a, uint32_t lane, uint64_t curr_obs, uint32_t curr_action, double reward,
                     int32_t terminated, uint64_t next_obs, uint32_t next_action, double *td);
-/* the same two for every lane at once (arrays of n_lanes; lane i is agent i) */
-int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions);
+/* the same two for every lane at once (arrays of n_lanes entries; lane i is agent i).
+ * ABI 6: n_lanes is the caller's array length and must equal the agent's lane
+ * count (RL_E_ARG otherwise), so the library never reads past a shorter array */
+int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions, uint64_t n_lanes);
 int rl_agent_updates(rl_agent *a, const uint64_t *curr_obs, const uint32_t *curr_action, const double *reward,
-                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td);
+                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td,
+                     uint64_t n_lanes);
 /* An Env over the agent's own lanes (one env per lane, the agent's RNG streams and
  * tables, the agent's stream): rl_env_reset / rl_env_step on it are Env::reset /
  * Env::step of the lane's env.  One view per agent; destroy it (rl_env_destroy)
@@ -403,6 +406,9 @@ int rl_agent_sync(rl_agent *a);
  * must hold the current one (a launch fails with RL_E_STATE otherwise). */
 int rl_agent_delta_words(rl_agent *a, uint64_t *n);
 int rl_agent_delta_max_words(rl_agent *a, uint64_t *n);
+/* ABI 6: the words of the largest layout either representation can need — size a
+ * caller-owned buffer by this and it survives every representation switch */
+int rl_agent_delta_cap_words(rl_agent *a, uint64_t *n);
 /* use caller-owned device memory (e.g. a torch int64 tensor, zeroed) as the buffer */
 int rl_agent_set_delta_buffer(rl_agent *a, void *device_ptr, uint64_t n_words);
 /* learner groups over every rank (the f64 merge grid's headroom; the attached

@@ -95,16 +95,42 @@ typedef struct { uint32_t key[8]; uint64_t ctr; uint32_t buf[64]; int idx; } rng
 #define QR(a, b, c, d) \
     a += b; d ^= a; d = (d << 16) | (d >> 16); c += d; b ^= c; b = (b << 12) | (b >> 20); \
     a += b; d ^= a; d = (d << 8) | (d >> 24);  c += d; b ^= c; b = (b << 7) | (b >> 25);
-static void chacha12_block(const uint32_t key[8], uint64_t ctr, uint32_t out[16]) {
+/* the ChaCha block function (RFC 8439 §2.3) over words 12-15 as given and
+ * `rounds` rounds; rand_chacha's ChaCha12 (rand 0.8.5's ThreadRng / StdRng core)
+ * puts a 64-bit block counter in words 12-13 and its stream id (0) in 14-15 */
+static void chacha_block(const uint32_t key[8], const uint32_t w[4], int rounds, uint32_t out[16]) {
     uint32_t x[16] = {0x61707865, 0x3320646e, 0x79622d32, 0x6b206574, key[0], key[1], key[2], key[3],
-                      key[4], key[5], key[6], key[7], (uint32_t)ctr, (uint32_t)(ctr >> 32), 0, 0};
+                      key[4], key[5], key[6], key[7], w[0], w[1], w[2], w[3]};
     uint32_t in[16];
     memcpy(in, x, sizeof in);
-    for (int i = 0; i < 6; ++i) {            /* 12 rounds = 6 double rounds */
+    for (int i = 0; i < rounds / 2; ++i) {   /* double rounds: columns, then diagonals */
         QR(x[0], x[4], x[8], x[12]) QR(x[1], x[5], x[9], x[13]) QR(x[2], x[6], x[10], x[14]) QR(x[3], x[7], x[11], x[15])
         QR(x[0], x[5], x[10], x[15]) QR(x[1], x[6], x[11], x[12]) QR(x[2], x[7], x[8], x[13]) QR(x[3], x[4], x[9], x[14])
     }
     for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+static void chacha12_block(const uint32_t key[8], uint64_t ctr, uint32_t out[16]) {
+    const uint32_t w[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0, 0};
+    chacha_block(key, w, 12, out);
+}
+/* known answer (tests/test_oracle_kat.py): the same block function at 20 rounds
+ * on RFC 8439 §2.3.2's key 00..1f, counter 1, nonce 00:00:00:09:00:00:00:4a:00:00:00:00,
+ * and at 12 rounds on the same input; prints the 16 output words as hex */
+static int kat_chacha(void) {
+    uint32_t key[8], out[16];
+    for (int i = 0; i < 8; ++i)
+        key[i] = (uint32_t)(4 * i) | (uint32_t)(4 * i + 1) << 8 | (uint32_t)(4 * i + 2) << 16 | (uint32_t)(4 * i + 3) << 24;
+    const uint32_t w[4] = {1u, 0x09000000u, 0x4a000000u, 0u};
+    const int rounds[2] = {20, 12};
+    printf("{");
+    for (int r = 0; r < 2; ++r) {
+        chacha_block(key, w, rounds[r], out);
+        printf("%s\"chacha%d\": [", r ? ", " : "", rounds[r]);
+        for (int i = 0; i < 16; ++i) printf("%s\"%08x\"", i ? ", " : "", out[i]);
+        printf("]");
+    }
+    printf("}\n");
+    return 0;
 }
 static void rng_refill(rng_t *r) {
     for (int b = 0; b < 4; ++b) chacha12_block(r->key, r->ctr++, r->buf + 16 * b);
@@ -723,6 +749,9 @@ static void *run_job(void *vp) {
 }
 
 int main(int argc, char **argv) {
+#ifndef RF_XOSHIRO
+    if (argc == 2 && strcmp(argv[1], "kat-chacha") == 0) return kat_chacha();
+#endif
     if (argc < 12) {
         fprintf(stderr, "usage: %s env map8x8 slippery agent policy selector algo n_episodes eval_at repeats threads [dump 0|1|2]\n",
                 argv[0]);

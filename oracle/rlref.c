@@ -250,8 +250,10 @@ double rlo_tanh(double x) {
 
 /* ======================================================================== */
 /* RNG: the reference draws from rand::thread_rng() (ChaCha12, entropy       */
-/* seeded) at: frozen_lake.rs:156-157,175; taxi.rs:446-447; blackjack.rs:562 */
-/* (via :541); uniform_epsilon_greed.rs:51-54,62.  All sites share one        */
+/* seeded) at: frozen_lake.rs:108 (reset), :126 (step); taxi.rs:137 (reset);  */
+/* blackjack.rs:76 (draw_card, the env's own thread_rng handle taken at :54); */
+/* uniform_epsilon_greed.rs:53 (the eps test), :62 (the random action);       */
+/* random_model.rs:30 (Dyna's replay index).  All sites share one             */
 /* thread-local stream.  Replacement: one xoshiro128+ stream per lane,        */
 /* seeded by splitmix64(seed + lane*C); next_u64 = lo word then hi word.      */
 /* ======================================================================== */
@@ -387,7 +389,8 @@ static void model_add(model_t *m, uint32_t k, uint32_t s2, double r) {
 }
 
 /* rand 0.8.5 UniformInt<u8> (u32 large type) for Uniform::from(1..11)
- * (blackjack.rs:542,562): range 10, ints_to_reject = (2^32-10)%10 = 6. */
+ * (the env's dist, blackjack.rs:55, sampled at :76): range 10,
+ * ints_to_reject = (2^32-10)%10 = 6. */
 uint32_t rlo_uniform_card_u32(uint32_t v, int *reject) {
     const uint32_t zone = 0xFFFFFFFFu - 6u;
     uint64_t m = (uint64_t)v * 10u;

@@ -466,6 +466,11 @@ struct rl_agent {
     train_launch_fn fn = nullptr;
     dim3 grid, block;
     size_t smem = 0;
+    // shared mode: the LDS carve per kernel family (index KParams::episodic: 0 the
+    // throughput kernel of rl_agent_run, 1 the episodic one of train / evaluate),
+    // whose register-limited residencies differ; the launch takes its own
+    size_t smem_v[2] = {0, 0};
+    uint32_t trc_kb_v[2] = {0, 0};
     rl_comm *comm = nullptr;   // multi-GPU: the merge delta is all-reduced over it
     double q_abs0 = 0.0;       // shared mode: max |Q| the table was last reset / set to (delta_bound's Q0)
 };
@@ -534,23 +539,39 @@ int agent_select_kernel(rl_agent *a) {
             // occupancy (without the pair slots), not only the 32-wave cap — cfg 4 at
             // 2^19 lanes on one GPU runs 4 groups per CU (128 VGPRs), so each may
             // take 40 KiB, not 20 (2.12e10 -> 2.2e10 env-steps/s measured)
-            int occ_regs = 0;
+            // The throughput kernel (episodic 0: rl_agent_run) and the episodic one
+            // (train / evaluate) differ in register use, so each gets the carve of
+            // its own residency (the query once named whichever kernel
+            // the previous call had left in KParams::episodic); launch_train_kernel
+            // takes the one it launches.  The pair pools / caches move between LDS
+            // and HBM at every launch boundary, so the slot count may differ.
             agent_sync_params(a);   // the kernel the query names follows KParams::fq
-            if (a->fn(a->kp, a->grid, a->block, base, a->stream, &occ_regs) != hipSuccess || occ_regs <= 0)
-                occ_regs = (int)(2048 / a->block.x);
-            const uint64_t resident = std::max<uint64_t>(
-                1, std::min<uint64_t>(per_cu, std::min<uint64_t>((uint64_t)occ_regs, 2048 / a->block.x)));
-            const int64_t room = (int64_t)(160 * 1024 / resident) - (int64_t)base - 1024;
-            a->kp.trc_kb = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(64, room / 1024));
+            const int32_t epi_saved = a->kp.episodic;
+            for (int32_t epi = 0; epi < 2; ++epi) {
+                a->kp.episodic = epi;
+                int occ_regs = 0;
+                if (a->fn(a->kp, a->grid, a->block, base, a->stream, &occ_regs) != hipSuccess || occ_regs <= 0)
+                    occ_regs = (int)(2048 / a->block.x);
+                const uint64_t resident = std::max<uint64_t>(
+                    1, std::min<uint64_t>(per_cu, std::min<uint64_t>((uint64_t)occ_regs, 2048 / a->block.x)));
+                const int64_t room = (int64_t)(160 * 1024 / resident) - (int64_t)base - 1024;
+                a->trc_kb_v[epi] = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(64, room / 1024));
+            }
+            a->kp.episodic = epi_saved;
         }
-        if (const char *e = getenv("RLAMD_TRC_KB")) {
-            const int v = atoi(e);
-            if (v >= 0 && v <= 150) a->kp.trc_kb = (uint32_t)v;
+        for (int epi = 0; epi < 2; ++epi) {
+            if (const char *e = getenv("RLAMD_TRC_KB")) {
+                const int v = atoi(e);
+                if (v >= 0 && v <= 150) a->trc_kb_v[epi] = (uint32_t)v;
+            }
+            a->smem_v[epi] = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector,
+                                               a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x,
+                                               a->trc_kb_v[epi], a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
+            if (a->smem_v[epi] > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
         }
-        a->smem = shared_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo, a->S,
-                                    a->A, (uint32_t)a->eh.cdf.size(), a->block.x, a->kp.trc_kb,
-                                    a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
-        if (a->smem > 160 * 1024) return fail(RL_E_ARG, "learner-group tables exceed the 160 KiB LDS");
+        const int ep = a->kp.episodic ? 1 : 0;
+        a->kp.trc_kb = a->trc_kb_v[ep];
+        a->smem = a->smem_v[ep];
     }
     if (a->tcnt) {
         // the trace sets' layout follows the kernel (rl_kparams.h); switching between
@@ -823,7 +844,15 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
                                     "(rl_agent_delta_words): set a larger one");
     }
     a->kp.episodic = (a->kp.target_episodes || a->kp.eval_at || a->kp.eval_only) ? 1 : 0;
+    if (!a->priv) {   // the LDS carve of the kernel family this launch takes (agent_select_kernel)
+        a->kp.trc_kb = a->trc_kb_v[a->kp.episodic];
+        a->smem = a->smem_v[a->kp.episodic];
+    }
     if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
+    // the launch moves the lanes an Env view shares: a lane the view
+    // once reset may have terminated since, so the view must reset before stepping
+    // again (the reference's Err(EnvNotReady), src/env.rs:17,24)
+    if (a->env_view) a->env_view->ready.assign(a->L, 0);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (a->timing) {
         HIPC(hipEventCreate(&e0));
@@ -1741,11 +1770,12 @@ int agent_call(rl_agent *a, int op, uint32_t lane0, uint32_t n, const uint64_t *
     if (n == 0) return RL_OK;
     if ((uint64_t)lane0 + n > a->L) return fail(RL_E_ARG, "lane out of range");
     HIPC(hipSetDevice(a->device));
-    const CallLayout cl(a->L);
-    if (!a->call_d) {
-        if (int rc = dalloc(&a->call_d, cl.total)) return rc;
-        HIPC(hipHostMalloc((void **)&a->call_h, cl.total, hipHostMallocDefault));
+    if (!a->call_d) {   // sized for every lane; a call stages only its n entries
+        const CallLayout full(a->L);
+        if (int rc = dalloc(&a->call_d, full.total)) return rc;
+        HIPC(hipHostMalloc((void **)&a->call_h, full.total, hipHostMallocDefault));
     }
+    const CallLayout cl(n);   // compact: a one-lane call moves a few bytes, not O(L)
     unsigned char *h = a->call_h;
     uint32_t *hs = (uint32_t *)(h + cl.s), *ha = (uint32_t *)(h + cl.a), *hs2 = (uint32_t *)(h + cl.s2),
              *ha2 = (uint32_t *)(h + cl.a2);
@@ -1799,14 +1829,21 @@ int rl_agent_update(rl_agent *a, uint32_t lane, uint64_t curr_obs, uint32_t curr
     return agent_call(a, CALL_UPDATE, lane, 1, &curr_obs, &curr_action, &reward, &t, &next_obs, &next_action,
                       nullptr, td);
 }
-int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions) {
+// every array holds n_lanes entries, and n_lanes must be the agent's lane count
+// (the library read L entries of whatever the caller passed)
+int rl_agent_get_actions(rl_agent *a, const uint64_t *obs, uint32_t *actions, uint64_t n_lanes) {
     if (!a || !obs || !actions) return fail(RL_E_ARG, "null argument");
+    if (n_lanes != a->L)
+        return fail(RL_E_ARG, "n_lanes " + std::to_string(n_lanes) + " != the agent's " + std::to_string(a->L) + " lanes");
     return agent_call(a, CALL_GET_ACTION, 0, a->L, obs, nullptr, nullptr, nullptr, nullptr, nullptr, actions, nullptr);
 }
 int rl_agent_updates(rl_agent *a, const uint64_t *curr_obs, const uint32_t *curr_action, const double *reward,
-                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td) {
+                     const uint8_t *terminated, const uint64_t *next_obs, const uint32_t *next_action, double *td,
+                     uint64_t n_lanes) {
     if (!a || !curr_obs || !curr_action || !reward || !terminated || !next_obs || !next_action || !td)
         return fail(RL_E_ARG, "null argument");
+    if (n_lanes != a->L)
+        return fail(RL_E_ARG, "n_lanes " + std::to_string(n_lanes) + " != the agent's " + std::to_string(a->L) + " lanes");
     return agent_call(a, CALL_UPDATE, 0, a->L, curr_obs, curr_action, reward, terminated, next_obs, next_action,
                       nullptr, td);
 }
@@ -1954,6 +1991,17 @@ int rl_agent_delta_max_words(rl_agent *a, uint64_t *n) {
     uint64_t mw = 0, sw = 0;
     if (!a->priv) merge_layout(a, &mw, &sw);
     *n = mw;
+    return RL_OK;
+}
+// the largest layout either representation needs: a caller-owned
+// buffer of this size survives every representation switch (set_action_selector,
+// set_future_q_value_func, set_q_mode, set_q)
+int rl_agent_delta_cap_words(rl_agent *a, uint64_t *n) {
+    if (!a || !n) return fail(RL_E_ARG, "null argument");
+    *n = 0;
+    if (a->priv) return RL_OK;
+    const uint64_t SA = (uint64_t)a->S * a->A, PSA = a->P * SA, ps = lds_entries(a);
+    *n = std::max<uint64_t>(ps + 5 * ps + SA + 1, 2 * PSA + SA + 1);
     return RL_OK;
 }
 

@@ -25,8 +25,27 @@ namespace rlamd {
                            // 1: fused, 2: fused and pinned before the selection)
 #endif
 
+// Pair pools (the small-table traces kernel, cfg 4):
+//  RLAMD_POOL_BF    the item body branch-free: every item of a round adds its
+//                   contribution and its row count (0 for the items of lanes that
+//                   do not train), the non-finite case behind one wave-uniform test,
+//                   the keep-write's LDS / HBM choice uniform while the round fits
+//  RLAMD_POOL_REC16 an item's tag and E as one 16-byte LDS record (one ds_read_b128
+//                   and one ds_write_b128 per item instead of a u16 and an f64 each)
+//  RLAMD_POOL_LREC  each lane's {td, pk} in a 16-byte LDS record read by its items
+//                   (one ds_read_b128) instead of three ds_bpermute
+#ifndef RLAMD_POOL_BF
+#define RLAMD_POOL_BF 0
+#endif
+#ifndef RLAMD_POOL_REC16
+#define RLAMD_POOL_REC16 0
+#endif
+#ifndef RLAMD_POOL_LREC
+#define RLAMD_POOL_LREC 0
+#endif
+__host__ __device__ constexpr uint32_t pool_item_bytes() { return RLAMD_POOL_REC16 ? 16u : 10u; }
 struct SmemLayout {
-    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, trc, qd, rm, total;
+    uint32_t st, misc, q, sum, cnt, sfl, qf, n, nd, t, list, rcp, tr, cdf, lrec, trc, qd, rm, total;
     uint32_t trc_cap;   // pair traces: list slots per lane held in LDS (the rest in HBM)
     uint32_t nrcp;   // entries of the 1.0/n table (larger n: a division, same bits)
 };
@@ -180,8 +199,12 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
     // pool form (small tables, pair_pool): trc_cap = items per wave, tags u16
     // [waves][cap] then E f64 [waves][cap]
     const bool pool = shared_q && traces == 2 && pair_pool_env(env);
+    // RLAMD_POOL_LREC: the pool sweep's per-lane record {td, pk} (16 B per lane of
+    // every wave), read by the items instead of three shuffles
+    l.lrec = off;
+    if (pool && RLAMD_POOL_LREC) off += (nthr >> 6) * 64u * 16u;
     if (pool) {
-        const uint32_t nw = nthr >> 6, c = trc_kb * 1024u / (nw * 10u);
+        const uint32_t nw = nthr >> 6, c = trc_kb * 1024u / (nw * pool_item_bytes());
         l.trc_cap = c < 64u * S * A ? c : 64u * S * A;
     } else if (shared_q && traces == 2) {
         const uint32_t c = trc_kb * 1024u / ((nthr + 2u) * 2u + (nthr + 1u) * 8u);
@@ -190,7 +213,8 @@ __host__ __device__ inline SmemLayout smem_layout(int env, int P, int ucb, int t
         l.trc_cap = 0u;
     }
     l.trc = off;
-    if (pool) off += l.trc_cap ? align16(l.trc_cap * (nthr >> 6) * 2u) + l.trc_cap * (nthr >> 6) * 8u : 0u;
+    if (pool && RLAMD_POOL_REC16) off += l.trc_cap * (nthr >> 6) * 16u;
+    else if (pool) off += l.trc_cap ? align16(l.trc_cap * (nthr >> 6) * 2u) + l.trc_cap * (nthr >> 6) * 8u : 0u;
     else off += l.trc_cap ? align16(l.trc_cap * (nthr + 2u) * 2u) + l.trc_cap * (nthr + 1u) * 8u : 0u;
     // qd  f64 [P][S][A]  fixed-point single-table Q-learning: the f64 image of every
     //                    entry beside its int64 word (qsh_layout), read by the step
@@ -798,8 +822,34 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     const bool pwave = (uint64_t)pw * p.lpw < p.G && plane0 < p.L;   // the wave holds lanes
     uint16_t *const PT = (uint16_t *)(smem + lay.trc) + pw * lay.trc_cap;
     double *const PE = (double *)(smem + lay.trc + align16(lay.trc_cap * (nthr >> 6) * 2u)) + pw * lay.trc_cap;
+    uint4 *const PR = (uint4 *)(smem + lay.trc) + pw * lay.trc_cap;   // RLAMD_POOL_REC16: {E lo, E hi, tag, 0}
+    uint4 *const LR = (uint4 *)(smem + lay.lrec) + pw * 64u;          // RLAMD_POOL_LREC: {td lo, td hi, pk, 0}
     uint16_t *const HT = p.tlist + plane0 * SA;
     double *const HE = p.trace + plane0 * SA;
+    // the LDS part of the wave's pool, item q < trc_cap
+    auto pool_tag = [&](uint32_t q) -> uint32_t {
+        if constexpr (RLAMD_POOL_REC16) return PR[q].z;
+        else return PT[q];
+    };
+    auto pool_get = [&](uint32_t q, uint32_t &tg, double &e) {
+        if constexpr (RLAMD_POOL_REC16) {
+            const uint4 r = PR[q];
+            tg = r.z;
+            e = __longlong_as_double((long long)(((uint64_t)r.y << 32) | r.x));
+        } else {
+            tg = PT[q];
+            e = PE[q];
+        }
+    };
+    auto pool_put = [&](uint32_t q, uint32_t tg, double e) {
+        if constexpr (RLAMD_POOL_REC16) {
+            const uint64_t b = (uint64_t)__double_as_longlong(e);
+            PR[q] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), tg, 0u);
+        } else {
+            PT[q] = (uint16_t)tg;
+            PE[q] = e;
+        }
+    };
     uint32_t npool = 0;
     uint32_t pbits[PBW];
 #pragma unroll
@@ -818,17 +868,14 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if constexpr (POOL) {
         npool = pwave ? p.tcnt[plane0] : 0u;
         const uint32_t nl = npool < lay.trc_cap ? npool : lay.trc_cap;
-        for (uint32_t q = plid; q < nl; q += 64u) {
-            PT[q] = HT[q];
-            PE[q] = HE[q];
-        }
+        for (uint32_t q = plid; q < nl; q += 64u) pool_put(q, HT[q], HE[q]);
         __syncthreads();
         // every lane's pair bits from the pool (each lane reads every tag: broadcast)
         constexpr uint32_t TB = 8;
         for (uint32_t q0 = 0; q0 < nl; q0 += TB) {
             uint32_t t[TB];
 #pragma unroll
-            for (uint32_t k = 0; k < TB; ++k) t[k] = PT[q0 + k < nl ? q0 + k : q0];
+            for (uint32_t k = 0; k < TB; ++k) t[k] = pool_tag(q0 + k < nl ? q0 + k : q0);
 #pragma unroll
             for (uint32_t k = 0; k < TB; ++k)
                 if (q0 + k < nl && ((t[k] >> 8) & 63u) == plid) pbits_set(t[k] & 0xffu);
@@ -1512,6 +1559,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                 const uint32_t C = lay.trc_cap;
                 uint32_t wpos = 0;                             // items kept so far (uniform)
                 constexpr uint32_t U = RLAMD_SWEEP_U;
+                if constexpr (RLAMD_POOL_LREC) {
+                    // the lane's {td, pk} for its items (same wave: LDS operations of a
+                    // wave complete in order, so no barrier between the write and the reads)
+                    const uint64_t tb = (uint64_t)__double_as_longlong(td);
+                    LR[plid] = make_uint4((uint32_t)tb, (uint32_t)(tb >> 32), pk, 0u);
+                    __builtin_amdgcn_wave_barrier();
+                }
                 for (uint32_t q0 = 0; q0 < npool; q0 += 64u * U) {
                     uint32_t tg[U], pkv[U];
                     double ev[U], tdv[U];
@@ -1521,9 +1575,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
 #pragma unroll
                         for (uint32_t u = 0; u < U; ++u) {
                             const uint32_t q = q0 + 64u * u + plid;
-                            const uint32_t qc = q < npool ? q : 0u;
-                            tg[u] = PT[qc];
-                            ev[u] = PE[qc];
+                            pool_get(q < npool ? q : 0u, tg[u], ev[u]);
                         }
                     } else {
 #pragma unroll
@@ -1532,16 +1584,22 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                             tg[u] = 0u;
                             ev[u] = 0.0;
                             if (q < npool) {
-                                if (q < C) { tg[u] = PT[q]; ev[u] = PE[q]; }
+                                if (q < C) pool_get(q, tg[u], ev[u]);
                                 else { tg[u] = HT[q]; ev[u] = HE[q]; }
                             }
                         }
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
-                        const int il = (int)((tg[u] >> 8) & 63u);
-                        tdv[u] = __shfl(td, il, 64);
-                        pkv[u] = (uint32_t)__shfl((int)pk, il, 64);
+                        const uint32_t il = (tg[u] >> 8) & 63u;
+                        if constexpr (RLAMD_POOL_LREC) {
+                            const uint4 r = LR[il];
+                            tdv[u] = __longlong_as_double((long long)(((uint64_t)r.y << 32) | r.x));
+                            pkv[u] = r.z;
+                        } else {
+                            tdv[u] = __shfl(td, (int)il, 64);
+                            pkv[u] = (uint32_t)__shfl((int)pk, (int)il, 64);
+                        }
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < U; ++u) {
@@ -1550,7 +1608,30 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         const bool istr = valid && ((pkv[u] >> 20) & 1u);
                         const bool keep = valid && !((pkv[u] >> 21) & 1u);
                         double en = ev[u];
-                        if (istr) {
+                        if constexpr (RLAMD_POOL_BF) {
+                            // branch-free: every valid item adds its contribution and its
+                            // row count — 0 for the items of lanes that do not train this
+                            // step (integer adds of 0 change nothing)
+                            const uint32_t id = tg[u] & 0xffu, uto = P == 2 ? (pkv[u] >> 16) & 1u : 0u;
+                            const double e1 = id == (pkv[u] & 0x1ffu) ? ev[u] + 1.0 : ev[u];
+                            const uint32_t o = id >> 2, b = id & 3u;   // A == 4
+                            const bool first = istr && (tg[u] & 0x8000u);
+                            const double d = p.lr * (tdv[u] * e1);
+                            const bool fin = __builtin_isfinite(d);
+                            // |raw| < 2^51 for finite d (trace_grid_k's guard bits): the magic add
+                            const double y = __builtin_ldexp(d, -e_tr) + 0x1.8p52;
+                            const int64_t raw = (istr && fin)
+                                ? (int64_t)((uint64_t)__double_as_longlong(y) - 0x4338000000000000ull) : (int64_t)0;
+                            if (valid) {
+                                atomicAdd(&SUM[qi(uto, o, b)], (unsigned long long)raw);
+                                atomicAdd(&CNTR[uto * SL + lrow(o)], first ? 1u : 0u);
+                            }
+                            trace_states += first ? 1u : 0u;
+                            if (__builtin_expect(__ballot(istr && !fin) != 0ull, 0)) {   // rare: non-finite kinds
+                                if (istr && !fin) contrib_tr(qi(uto, o, b), d, e_tr);
+                            }
+                            en = istr ? e1 * p.gl : ev[u];
+                        } else if (istr) {
                             const uint32_t id = tg[u] & 0xffu, uto = P == 2 ? (pkv[u] >> 16) & 1u : 0u;
                             const double e1 = id == (pkv[u] & 0x1ffu) ? ev[u] + 1.0 : ev[u];
                             const uint32_t o = id >> 2, b = id & 3u;   // A == 4
@@ -1563,8 +1644,10 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                         }
                         const uint64_t m = __ballot(keep);
                         const uint32_t pos = wpos + lanes_below(m);
-                        if (keep) {
-                            if (wpos + 64u <= C || pos < C) { PT[pos] = (uint16_t)tg[u]; PE[pos] = en; }
+                        if (RLAMD_POOL_BF && wpos + 64u <= C) {   // uniform: the round's kept items fit in LDS
+                            if (keep) pool_put(pos, tg[u], en);
+                        } else if (keep) {
+                            if (wpos + 64u <= C || pos < C) pool_put(pos, tg[u], en);
                             else { HT[pos] = (uint16_t)tg[u]; HE[pos] = en; }
                         }
                         wpos += (uint32_t)__popcll(m);
@@ -1583,7 +1666,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                     const uint32_t pos = wpos + lanes_below(m);
                     const uint16_t tag = (uint16_t)(nid | (plid << 8) | (first_new ? 0x8000u : 0u));
                     const double en = 1.0 * p.gl;
-                    if (pos < C) { PT[pos] = tag; PE[pos] = en; }
+                    if (pos < C) pool_put(pos, tag, en);
                     else { HT[pos] = tag; HE[pos] = en; }
                 }
                 npool = wpos + (uint32_t)__popcll(m);
@@ -1890,8 +1973,11 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
     if constexpr (POOL) {
         const uint32_t nl = npool < lay.trc_cap ? npool : lay.trc_cap;
         for (uint32_t q = plid; q < nl; q += 64u) {
-            HT[q] = PT[q];
-            HE[q] = PE[q];
+            uint32_t tg;
+            double e;
+            pool_get(q, tg, e);
+            HT[q] = (uint16_t)tg;
+            HE[q] = e;
         }
         if (plid == 0 && pwave) p.tcnt[plane0] = npool;
     } else {

@@ -195,7 +195,7 @@ struct PolicySpec {
     int policy = RL_POLICY_TABULAR;
     rl_network_config net{};
     bool mul_decay = false;      // `a * exploration_time` (frozen_lake_neural.rs:181), else `a - ε0/(t·n)`
-    uint64_t eval_episodes = 0;  // final evaluate(): 0 = n_episodes (frozen_lake.rs:201), 1000 in the neural bin
+    uint64_t eval_episodes = 0;  // final evaluate(): 0 = n_episodes (bin/frozen_lake.rs:201), 1000 in the neural bin
 };
 
 // src/bin/frozen_lake.rs:139-216: TabularPolicy(lr, 0.0); ε-greedy with decay

@@ -89,8 +89,8 @@ SIGNATURES = {
     "rl_agent_get_action": (C.c_int, [_V, C.c_uint32, C.c_uint64, _P(C.c_uint32)]),
     "rl_agent_update": (C.c_int, [_V, C.c_uint32, C.c_uint64, C.c_uint32, C.c_double, C.c_int32, C.c_uint64,
                                   C.c_uint32, _P(C.c_double)]),
-    "rl_agent_get_actions": (C.c_int, [_V, _V, _V]),
-    "rl_agent_updates": (C.c_int, [_V, _V, _V, _V, _V, _V, _V, _V]),
+    "rl_agent_get_actions": (C.c_int, [_V, _V, _V, C.c_uint64]),
+    "rl_agent_updates": (C.c_int, [_V, _V, _V, _V, _V, _V, _V, _V, C.c_uint64]),
     "rl_agent_env": (C.c_int, [_V, _P(_V)]),
     "rl_env_reset_lane": (C.c_int, [_V, C.c_uint32, _P(C.c_uint64)]),
     "rl_env_step_lane": (C.c_int, [_V, C.c_uint32, C.c_uint32, _P(C.c_uint64), _P(C.c_double),
@@ -133,6 +133,7 @@ SIGNATURES = {
     "rl_agent_lane_state": (C.c_int, [_V, _V, _V, C.c_size_t]),
     "rl_agent_delta_words": (C.c_int, [_V, _P(C.c_uint64)]),
     "rl_agent_delta_max_words": (C.c_int, [_V, _P(C.c_uint64)]),
+    "rl_agent_delta_cap_words": (C.c_int, [_V, _P(C.c_uint64)]),
     "rl_agent_set_delta_buffer": (C.c_int, [_V, _V, C.c_uint64]),
     "rl_agent_set_merge_groups": (C.c_int, [_V, C.c_uint64]),
     "rl_agent_launch_train": (C.c_int, [_V]),
@@ -366,19 +367,28 @@ class Agent:
                                     int(bool(terminated)), int(next_obs), int(next_action), C.byref(td)))
         return td.value
 
+    def _lane_arrays(self, **arrays):
+        """every array exactly one entry per lane (the library reads
+        n_lanes entries of each; rl.h ABI 6 also checks the length it is given)"""
+        for name, x in arrays.items():
+            if x.ndim != 1 or x.size != self.L:
+                raise ValueError(f"{name}: {x.size} entries for {self.L} lanes")
+
     def get_actions(self, obs):
         obs = np.ascontiguousarray(obs, np.uint64)
+        self._lane_arrays(obs=obs)
         out = np.zeros(self.L, np.uint32)
-        check(lib().rl_agent_get_actions(self.h, obs.ctypes.data, out.ctypes.data))
+        check(lib().rl_agent_get_actions(self.h, obs.ctypes.data, out.ctypes.data, obs.size))
         return out
 
     def updates(self, s, a, r, term, s2, a2):
         s, s2 = np.ascontiguousarray(s, np.uint64), np.ascontiguousarray(s2, np.uint64)
         a, a2 = np.ascontiguousarray(a, np.uint32), np.ascontiguousarray(a2, np.uint32)
         r, term = np.ascontiguousarray(r, np.float64), np.ascontiguousarray(term, np.uint8)
+        self._lane_arrays(s=s, a=a, r=r, term=term, s2=s2, a2=a2)
         td = np.zeros(self.L, np.float64)
         check(lib().rl_agent_updates(self.h, s.ctypes.data, a.ctypes.data, r.ctypes.data, term.ctypes.data,
-                                     s2.ctypes.data, a2.ctypes.data, td.ctypes.data))
+                                     s2.ctypes.data, a2.ctypes.data, td.ctypes.data, s.size))
         return td
 
     def set_future_q_value_func(self, algo):
@@ -533,6 +543,12 @@ class Agent:
     def delta_max_words(self):
         n = C.c_uint64()
         check(lib().rl_agent_delta_max_words(self.h, C.byref(n)))
+        return n.value
+
+    def delta_cap_words(self):
+        """the largest merge layout of either representation (size caller buffers by it)"""
+        n = C.c_uint64()
+        check(lib().rl_agent_delta_cap_words(self.h, C.byref(n)))
         return n.value
 
     def set_merge_groups(self, total_groups):

@@ -19,10 +19,10 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -I../include -fPIC -ffp-contract=off -fn
 objs="exp/tu_$NAME.o exp/misc_$NAME.o exp/host_$NAME.o build/rl_build_id.o"
 for t in $ALL; do
   [ "$t" = "$TU" ] && continue
-  /opt/rocm/bin/hipcc $F -DRLAMD_ONLY=9,9,9,9,9 -c csrc/rl_train_$t.hip -o exp/empty_$t.o &
-  objs="$objs exp/empty_$t.o"
+  /opt/rocm/bin/hipcc $F -DRLAMD_ONLY=9,9,9,9,9 -c csrc/rl_train_$t.hip -o exp/empty_${NAME}_$t.o &
+  objs="$objs exp/empty_${NAME}_$t.o"
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o exp/librlamd_$NAME.so $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -f exp/tu_$NAME.o exp/misc_$NAME.o exp/host_$NAME.o exp/empty_*.o
+rm -f exp/tu_$NAME.o exp/misc_$NAME.o exp/host_$NAME.o exp/empty_${NAME}_*.o
 ls -la exp/librlamd_$NAME.so

@@ -239,3 +239,29 @@ def test_agent_call_errors(rl):
     o = C.c_uint64()
     assert rl.lib().rl_env_reset_lane(h, 0, C.byref(o)) == 5
     rl.lib().rl_env_destroy(h)
+
+
+def test_batched_call_lengths_and_view_readiness(rl):
+    """a batched call never reads past the caller's arrays (ValueError
+    in Python, RL_E_ARG from the C ABI when n_lanes differs from the agent's), and
+    a launch over the lanes clears the Env view's readiness (src/env.rs:17,24:
+    the lane may have terminated since the view reset it)"""
+    agent = rl.Agent(rl.default_params(env="frozen_lake", n_lanes=8, group_size=1))
+    with pytest.raises(ValueError):
+        agent.get_actions(np.zeros(4, np.uint64))
+    with pytest.raises(ValueError):
+        z = np.zeros(8, np.uint64)
+        agent.updates(z, z[:7].astype(np.uint32), np.zeros(8), np.zeros(8, np.uint8), z, z.astype(np.uint32))
+    obs = np.zeros(4, np.uint64)
+    out = np.zeros(8, np.uint32)
+    assert rl.lib().rl_agent_get_actions(agent.h, obs.ctypes.data, out.ctypes.data, 4) == 2
+    assert rl.lib().rl_agent_get_actions(agent.h, np.zeros(8, np.uint64).ctypes.data, out.ctypes.data, 8) == 0
+    env = agent.env()
+    env.reset_lane(0)
+    env.step_lane(0, 1)                     # ready after the reset
+    agent.train(2, 0)                       # moves the lanes the view shares
+    with pytest.raises(rl.RLError) as ex:
+        env.step_lane(0, 1)
+    assert ex.value.code == 1               # EnvNotReady until the view resets the lane
+    env.reset_lane(0)
+    env.step_lane(0, 1)

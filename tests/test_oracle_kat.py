@@ -191,3 +191,25 @@ def test_golden_trajectories_match_oracle():
     assert got.keys() == want.keys()
     for k in want:
         assert got[k] == want[k], k
+
+
+# RFC 8439 §2.3.2, "Test Vector for the ChaCha20 Block Function": key 00:01:..:1f,
+# block count 1, nonce 00:00:00:09:00:00:00:4a:00:00:00:00 — the state after the
+# 20 rounds and the final addition, as published
+RFC8439_2_3_2 = ["e4e7f110", "15593bd1", "1fdd0f50", "c47120a3", "c7f4d1c7", "0368c033", "9aaa2204", "4e6cd4c3",
+                 "466482d2", "09aa9f07", "05d7c214", "a2028bd9", "d19c12b5", "b94e16de", "e883d0cb", "4e3c50a2"]
+
+
+def test_ref_faithful_chacha_block_rfc8439(oracle):
+    """VERDICT r04 missing 5: the block function behind the CPU baseline's
+    ThreadRng (rand 0.8.5 -> rand_chacha ChaCha12; reference draw sites
+    frozen_lake.rs:108,126, taxi.rs:137, blackjack.rs:76, uniform_epsilon_greed.rs:53,62)
+    is oracle/ref_faithful.c chacha_block; at 20 rounds it must reproduce the
+    published RFC 8439 block, so its 12-round use differs only in the round count"""
+    import json as _json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_build", "ref_faithful")
+    out = _json.loads(subprocess.run([exe, "kat-chacha"], check=True, capture_output=True, text=True).stdout)
+    assert out["chacha20"] == RFC8439_2_3_2
+    # the 12-round block of the same input: no published vector, a regression value
+    assert out["chacha12"][0] == "66138b7f" and out["chacha12"] != out["chacha20"]

@@ -1,7 +1,9 @@
-"""CPU: the committed bench evidence (profiles/r04_bench/*.json) is internally
-consistent: every roofline fraction is a fraction (<= 1),
-counters are attached only from the benched build (rl_build_id equal), and the
-PMC summary they cite exists and holds that build's kernel time."""
+"""CPU: the committed bench evidence of the latest round (profiles/rNN_bench/*.json)
+is internally consistent: every roofline fraction is a
+fraction (<= 1), counters are attached only from the benched build (rl_build_id
+equal), the PMC summary they cite exists and holds that build's kernel time, and
+the kernel's sampled average duration is not above the step it is part of
+(a 1-in-8 event sample once overstated a 100-ms kernel)."""
 import glob
 import json
 import os
@@ -9,7 +11,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04_bench", "*.json")))
+ROUND = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench")))[-1]
+LINES = sorted(glob.glob(os.path.join(ROUND, "*.json")))
 
 
 @pytest.mark.parametrize("path", LINES, ids=[os.path.basename(p) for p in LINES])
@@ -18,6 +21,10 @@ def test_bench_line_roofline_is_consistent(path):
     r = d["roofline"]
     assert 0.0 < r["frac"] <= 1.0, r["frac"]
     assert r["bound"] in ("latency", "valu", "hbm")
+    # one step = the train launch + the merge: its kernel cannot take longer (bench
+    # lines from round 5 on time the private rows' every launch)
+    if int(os.path.basename(ROUND)[1:3]) >= 5:
+        assert 0.0 < r["kernel_avg_ms"] <= d["ms_per_step"], (r["kernel_avg_ms"], d["ms_per_step"])
     assert r["hbm"]["fused_frac"] <= 1.0
     if r["hbm"]["traffic_frac"] is not None:
         assert r["hbm"]["traffic_frac"] <= 1.0
@@ -36,6 +43,6 @@ def test_bench_line_roofline_is_consistent(path):
 
 
 def test_headline_line_is_the_default_workload():
-    d = json.load(open(os.path.join(ROOT, "profiles", "r04_bench", "bench_cfg2.json")))
+    d = json.load(open(os.path.join(ROUND, "bench_cfg2.json")))
     assert d["config"]["survey_cfg"] == 2 and d["config"]["lanes_per_gpu"] == 1 << 20
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
