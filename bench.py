@@ -9,7 +9,8 @@ the merge (and, for N>1 GPUs, the ΔQ all-reduce over RCCL).  Defaults follow
 §8(d): warm-up 64 synchronous steps (1 launch), timed window 4,096 (64 launches).
 --config 3/4/5 selects the other §8(d) workloads (per-GPU lane counts); 6 and 7
 the §8(f) rows on private agents: frozen_lake_neural's NeuralPolicy and
-cliffwalking_model's Dyna-Q (InternalModelAgent, 10 planning steps).
+cliffwalking_model's Dyna-Q (InternalModelAgent, 10 planning steps); 8 is cfg 3's
+Taxi + UCB with Q-learning, where Q stays finite (UCB's ln / sqrt / divide timed).
 
   python bench.py [--gpus N --steps K --warmup W]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -50,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7, 8],
                     help="SURVEY §8(d) workload preset (2 = the headline)")
     ap.add_argument("--lanes", type=int, default=None, help="env lanes per GPU (weak scaling: per-GPU work fixed)")
     ap.add_argument("--lanes-total", type=int, default=None,
@@ -112,6 +113,13 @@ PRESETS = {
                                                 net_hidden=32, net_act1="leaky_relu6", net_act2="linear")),
     7: dict(env="cliff_walking", agent="one_step", policy="tabular", selector="eps_greedy", algo="qlearning",
             lanes=1 << 20, group=1, extra=dict(planning=10)),
+    # cfg 3's env and selector in a regime where Q stays finite:
+    # UCB + Q-learning takes max(q') as its target (src/agent.rs:27-32), so the
+    # selection's ln / sqrt / divide (upper_confidence_bound.rs:29-42) run on finite
+    # rows at every step; one-step tabular with a contracting target: the proven
+    # fixed point
+    8: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="qlearning",
+            lanes=1 << 20, group=512),
 }
 
 

@@ -434,8 +434,8 @@ struct rl_agent {
     int trace_layout = -1;   // layout_sparse_traces() of the kernel the trace sets were built for
     // Dyna model (private mode)
     uint32_t plan = 0;
-    uint32_t *mcnt = nullptr, *mkey = nullptr, *ms2 = nullptr, *mslot = nullptr;
-    double *mr = nullptr;
+    uint32_t *mcnt = nullptr, *mslot = nullptr;
+    uint4 *mrec = nullptr;
     // NeuralPolicy
     bool neural = false;
     uint32_t n_in = 0, n_params = 0, net_gen = 0xffffffffu;
@@ -826,7 +826,7 @@ void agent_sync_params(rl_agent *a) {
     p.n_groups = a->n_groups;
     p.psal = lds_entries(a);
     p.plan_steps = a->plan;
-    p.mcnt = a->mcnt; p.mkey = a->mkey; p.ms2 = a->ms2; p.mslot = a->mslot; p.mr = a->mr;
+    p.mcnt = a->mcnt; p.mrec = a->mrec; p.mslot = a->mslot;
     p.elog = a->elog_cap ? a->elog_d : nullptr;
     p.elog_cnt = a->elog_cnt_d;
     p.elog_cap = a->elog_cap;
@@ -1443,7 +1443,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->q_priv); dfree(a->n_priv); dfree(a->t_priv);
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
-    dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
+    dfree(a->mcnt); dfree(a->mrec); dfree(a->mslot);
     dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d); dfree(a->call_d);
     if (a->call_h) (void)hipHostFree(a->call_h);
     if (a->env_view) a->env_view->owner = nullptr;   // the view outlives its agent: calls fail with RL_E_STATE
@@ -1620,11 +1620,9 @@ int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
     }
     if (a->priv) {
         if (n < PSA * a->L) return fail(RL_E_ARG, "output too small: need n_lanes*P*S*A");
-        std::vector<double> tmp(PSA * a->L);
-        HIPC(hipMemcpyAsync(tmp.data(), a->q_priv, tmp.size() * 8, hipMemcpyDeviceToHost, a->stream));
+        // the device layout is the caller's, [L][P][S][A] (lane-major, rl_kparams.h)
+        HIPC(hipMemcpyAsync(out, a->q_priv, PSA * a->L * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
-        for (size_t e = 0; e < PSA; ++e)
-            for (size_t l = 0; l < a->L; ++l) out[l * PSA + e] = tmp[e * a->L + l];
         return RL_OK;
     }
     if (n < PSA) return fail(RL_E_ARG, "output too small: need P*S*A");
@@ -1643,10 +1641,7 @@ int rl_agent_set_q(rl_agent *a, const double *in, size_t n) {
     const size_t PSA = (size_t)a->P * a->S * a->A;
     if (a->priv) {
         if (n < PSA * a->L) return fail(RL_E_ARG, "input too small");
-        std::vector<double> tmp(PSA * a->L);
-        for (size_t e = 0; e < PSA; ++e)
-            for (size_t l = 0; l < a->L; ++l) tmp[e * a->L + l] = in[l * PSA + e];
-        HIPC(hipMemcpy(a->q_priv, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(a->q_priv, in, PSA * a->L * 8, hipMemcpyHostToDevice));   // [L][P][S][A] both sides
         return RL_OK;
     }
     if (n < PSA) return fail(RL_E_ARG, "input too small");
@@ -1694,12 +1689,9 @@ int rl_agent_get_ucb(rl_agent *a, uint64_t *counts, size_t nc, uint64_t *t, size
     const size_t SA = (size_t)a->S * a->A;
     if (a->priv) {
         if (nc < SA * a->L || nt < a->L) return fail(RL_E_ARG, "output too small");
-        std::vector<uint64_t> tmp(SA * a->L);
-        HIPC(hipMemcpyAsync(tmp.data(), a->n_priv, tmp.size() * 8, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipMemcpyAsync(counts, a->n_priv, SA * a->L * 8, hipMemcpyDeviceToHost, a->stream));   // [L][S][A]
         HIPC(hipMemcpyAsync(t, a->t_priv, a->L * 8, hipMemcpyDeviceToHost, a->stream));
         HIPC(hipStreamSynchronize(a->stream));
-        for (size_t e = 0; e < SA; ++e)
-            for (size_t l = 0; l < a->L; ++l) counts[l * SA + e] = tmp[e * a->L + l];
         return RL_OK;
     }
     if (nc < SA || nt < 1) return fail(RL_E_ARG, "output too small");
@@ -1718,10 +1710,7 @@ int rl_agent_set_ucb(rl_agent *a, const uint64_t *counts, size_t nc, const uint6
     for (size_t i = 0; i < n_t; ++i)
         if (t[i] == 0) return fail(RL_E_ARG, "UCB t starts at 1 (upper_confidence_bound.rs:20)");
     if (a->priv) {
-        std::vector<uint64_t> tmp(SA * a->L);   // [L][S][A] -> SoA [entry][lane]
-        for (size_t e = 0; e < SA; ++e)
-            for (size_t l = 0; l < a->L; ++l) tmp[e * a->L + l] = counts[l * SA + e];
-        HIPC(hipMemcpyAsync(a->n_priv, tmp.data(), tmp.size() * 8, hipMemcpyHostToDevice, a->stream));
+        HIPC(hipMemcpyAsync(a->n_priv, counts, SA * a->L * 8, hipMemcpyHostToDevice, a->stream));   // [L][S][A]
         HIPC(hipMemcpyAsync(a->t_priv, t, a->L * 8, hipMemcpyHostToDevice, a->stream));
     } else {
         HIPC(hipMemcpyAsync(a->n_base, counts, SA * 8, hipMemcpyHostToDevice, a->stream));
@@ -1914,15 +1903,14 @@ int rl_agent_set_planning(rl_agent *a, uint32_t planning_steps) {
     if (planning_steps && !a->priv) return fail(RL_E_ARG, "Dyna planning needs group_size 1 (private agents)");
     HIPC(hipSetDevice(a->device));
     HIPC(hipStreamSynchronize(a->stream));
-    dfree(a->mcnt); dfree(a->mkey); dfree(a->ms2); dfree(a->mslot); dfree(a->mr);
-    a->mcnt = a->mkey = a->ms2 = a->mslot = nullptr;
-    a->mr = nullptr;
+    dfree(a->mcnt); dfree(a->mrec); dfree(a->mslot);
+    a->mcnt = a->mslot = nullptr;
+    a->mrec = nullptr;
     a->plan = 0;
     if (planning_steps) {
         const size_t n = (size_t)a->S * a->A * a->L;
         int rc;
-        if ((rc = dalloc(&a->mcnt, a->L)) || (rc = dalloc(&a->mkey, n)) || (rc = dalloc(&a->ms2, n)) ||
-            (rc = dalloc(&a->mslot, n)) || (rc = dalloc(&a->mr, n)))
+        if ((rc = dalloc(&a->mcnt, a->L)) || (rc = dalloc(&a->mrec, n)) || (rc = dalloc(&a->mslot, n)))
             return rc;
         HIPC(hipMemset(a->mcnt, 0, (size_t)a->L * 4));
         HIPC(hipMemset(a->mslot, 0, n * 4));

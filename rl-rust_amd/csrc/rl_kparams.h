@@ -78,9 +78,11 @@ struct KParams {
     uint32_t psal;         // LDS-held entries per group (Blackjack eps-greedy: compact rows)
     uint64_t *qslot;       // [n_groups][psal] f64 bits
     uint32_t n_groups;
-    // private mode (SoA [entry][lane])
-    double *q_priv;
-    uint64_t *n_priv;      // [S*A][L]
+    // private mode, LANE-MAJOR (round 5): a lane's table is one
+    // contiguous block, so the row a step reads is one 16-byte-aligned run of A f64
+    // (entry-major [entry][lane] put every lane's 8-byte gather in its own 128-B line)
+    double *q_priv;        // [L][P][S][A]
+    uint64_t *n_priv;      // [L][S*A]
     uint64_t *t_priv;      // [L]
     // eligibility traces, per lane a sparse set of the episode's visited states:
     // tlist[j] = j-th visited state, slot_of[s] = its slot (valid iff
@@ -99,8 +101,8 @@ struct KParams {
     // sparse set in insertion order, entry j = (key = s*A+a, s', r)
     uint32_t plan_steps;
     uint32_t *mcnt;        // [L]
-    uint32_t *mkey, *ms2, *mslot;   // [S*A][L]
-    double *mr;            // [S*A][L]
+    uint4 *mrec;           // [L][S*A] entry j of a lane's model: {key = s*A+a, s', r lo, r hi} (16 B)
+    uint32_t *mslot;       // [L][S*A] slot of key (valid iff < mcnt and mrec[slot].x == key)
     // NeuralPolicy (private mode): per-lane 2-layer MLP, parameters SoA [param][lane]
     // in the order [W1 n_in x H][b1 H][W2 H x A][b2 A] (rl.h rl_agent_net_dims)
     double *net_w;         // [n_params][L]

@@ -41,7 +41,7 @@ namespace rlamd {
 #define RLAMD_POOL_REC16 0
 #endif
 #ifndef RLAMD_POOL_LREC
-#define RLAMD_POOL_LREC 0
+#define RLAMD_POOL_LREC 1
 #endif
 __host__ __device__ constexpr uint32_t pool_item_bytes() { return RLAMD_POOL_REC16 ? 16u : 10u; }
 struct SmemLayout {
@@ -2205,7 +2205,24 @@ struct PrivAgent {
         if (UCB) p.t_priv[lane] = t;
         if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
     }
-    __device__ __forceinline__ double &qref(uint32_t idx) const { return p.q_priv[(uint64_t)idx * Ls + lane]; }
+    // lane-major tables (rl_kparams.h): the lane's Q block [P][S][A], its UCB counts [S][A]
+    __device__ __forceinline__ double &qref(uint32_t idx) const { return p.q_priv[lane * (uint64_t)(P * SA) + idx]; }
+    __device__ __forceinline__ uint64_t &nref(uint32_t idx) const { return p.n_priv[lane * (uint64_t)SA + idx]; }
+    // row s of table tbl: A consecutive f64, 16-byte aligned (P*S*A and A even for every env)
+    __device__ __forceinline__ void row(uint32_t tbl, uint32_t s, double (&v)[A]) const {
+        if constexpr (A % 2 == 0) {
+            const double2 *r = (const double2 *)__builtin_assume_aligned(&qref(tbl * SA + s * A), 16);
+#pragma unroll
+            for (int i = 0; i < A / 2; ++i) {
+                const double2 x = r[i];
+                v[2 * i] = x.x;
+                v[2 * i + 1] = x.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < A; ++i) v[i] = qref(tbl * SA + s * A + i);
+        }
+    }
     // Policy::predict (tabular_policy.rs:27-29, double_tabular_policy.rs:31-40, neural_policy.rs:43-47)
     __device__ __forceinline__ void predict(uint32_t s, double (&v)[A]) {
         if constexpr (NEURAL) {
@@ -2214,10 +2231,12 @@ struct PrivAgent {
             for (int i = 0; i < A; ++i) v[i] = nc.y[i];
             return;
         }
+        row(0u, s, v);
+        if constexpr (P == 2) {
+            double w[A];
+            row(1u, s, w);
 #pragma unroll
-        for (int i = 0; i < A; ++i) {
-            if constexpr (P == 1) v[i] = qref(s * A + i);
-            else v[i] = (qref(s * A + i) + qref(SA + s * A + i)) / 2.0;
+            for (int i = 0; i < A; ++i) v[i] = (v[i] + w[i]) / 2.0;
         }
     }
     // Policy::get_values of table `tbl` (double policy: flag ? alpha : beta)
@@ -2225,8 +2244,7 @@ struct PrivAgent {
         if constexpr (NEURAL) {
             predict(s, v);
         } else {
-#pragma unroll
-            for (int i = 0; i < A; ++i) v[i] = qref(tbl * SA + s * A + i);
+            row(tbl, s, v);
         }
     }
     // Policy::update with x = td (one-step) or td * E[o][b] (traces)
@@ -2250,9 +2268,9 @@ struct PrivAgent {
             double u[A];
 #pragma unroll
             for (int i = 0; i < A; ++i)
-                u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)p.n_priv[(uint64_t)(s * A + i) * Ls + lane]);
+                u[i] = ucb_value(v[i], p.ucb_c, lnt, (double)nref(s * A + i));
             const uint32_t a = argmax<A>(u);
-            p.n_priv[(uint64_t)(s * A + a) * Ls + lane] += 1ull;
+            nref(s * A + a) += 1ull;
             t += 1;
             return a;
         }
@@ -2274,7 +2292,7 @@ struct PrivAgent {
                 double sum = 0.0;
 #pragma unroll
                 for (int i = 0; i < A; ++i) {
-                    pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)p.n_priv[(uint64_t)(s2 * A + i) * Ls + lane]);
+                    pr[i] = ucb_value(q2[i], p.ucb_c, lnt, (double)nref(s2 * A + i));
                     sum += pr[i];
                 }
 #pragma unroll
@@ -2317,20 +2335,22 @@ struct PrivAgent {
         if (p.plan_steps) {
             uint32_t mc = p.mcnt[lane];
             const uint32_t key = s * A + a;
-            const uint32_t j0 = p.mslot[(uint64_t)key * Ls + lane];
-            if (!(j0 < mc && p.mkey[(uint64_t)j0 * Ls + lane] == key)) {
-                p.mkey[(uint64_t)mc * Ls + lane] = key;
-                p.ms2[(uint64_t)mc * Ls + lane] = s2;
-                p.mr[(uint64_t)mc * Ls + lane] = r;
-                p.mslot[(uint64_t)key * Ls + lane] = mc;
+            uint4 *const mrec = p.mrec + lane * (uint64_t)SA;     // the lane's model, lane-major
+            uint32_t *const mslot = p.mslot + lane * (uint64_t)SA;
+            const uint32_t j0 = mslot[key];
+            if (!(j0 < mc && mrec[j0].x == key)) {
+                const uint64_t rb = (uint64_t)__double_as_longlong(r);
+                mrec[mc] = make_uint4(key, s2, (uint32_t)rb, (uint32_t)(rb >> 32));
+                mslot[key] = mc;
                 ++mc;
                 p.mcnt[lane] = mc;
             }
             for (uint32_t i = 0; i < p.plan_steps; ++i) {
                 const uint32_t j = gen_index(L.rng, mc);
-                const uint32_t pk = p.mkey[(uint64_t)j * Ls + lane];
-                const uint32_t ps2 = p.ms2[(uint64_t)j * Ls + lane];
-                const double pr = p.mr[(uint64_t)j * Ls + lane];
+                const uint4 m = mrec[j];                         // one 16-byte read
+                const uint32_t pk = m.x;
+                const uint32_t ps2 = m.y;
+                const double pr = __longlong_as_double((long long)(((uint64_t)m.w << 32) | m.z));
                 const uint32_t na = select(ps2);
                 update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
             }

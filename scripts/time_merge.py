@@ -41,8 +41,8 @@ def timed(stream, fn, n=N):
     return e0.elapsed_time(e1) / n, (t1 - t0) * 1e3 / n
 
 
-def one(cfg):
-    kw = bench_params(cfg, {})
+def one(cfg, lanes=None):
+    kw = bench_params(cfg, {"n_lanes": lanes} if lanes else {})
     a = rl.Agent(rl.default_params(**{k: v for k, v in kw.items() if k != "reset_step"}))
     a.set_reset_step(bool(kw["reset_step"]))
     s = torch.cuda.Stream()
@@ -75,6 +75,8 @@ def one(cfg):
 
 
 if __name__ == "__main__":
-    cfgs = [int(x) for x in sys.argv[1:]] or [2, 3, 4, 5]
+    # cfg or cfg:lanes (2:131072 = the north star's 2^20 lanes over 8 GPUs, one rank's shard)
+    cfgs = sys.argv[1:] or ["2", "3", "4", "5", "2:131072"]
     for c in cfgs:
-        print(json.dumps(one(c)), flush=True)
+        cf, _, ln = c.partition(":")
+        print(json.dumps(one(int(cf), int(ln) if ln else None)), flush=True)

@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 LAUNCHES = 2
 SYNC = 64
 CASES = {"cfg2": (2, {}), "cfg2_slippery": (2, {"slippery": 1}), "cfg3": (3, {}), "cfg4": (4, {}),
-         "cfg5": (5, {}),
+         "cfg5": (5, {}), "cfg8": (8, {}),
          # BASELINE's whole cfg 4 (2^19 lanes) on one GPU, as bench.py --config 4 --lanes 524288
          "cfg4_2p19": (4, {"n_lanes": 1 << 19})}
 

@@ -27,10 +27,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
-LAUNCHES = {"cfg2": 65, "cfg2_slippery": 65, "cfg3": 65, "cfg4": 65, "cfg5": 65, "cfg4_2p19": 65}
+LAUNCHES = {"cfg2": 65, "cfg2_slippery": 65, "cfg3": 65, "cfg4": 65, "cfg5": 65, "cfg4_2p19": 65, "cfg8": 65}
 # name -> (SURVEY cfg, extra bench.py arguments); cfg 2 is the headline (the
 # proven fixed point, k_train_shared_o8: VERDICT r03 item 3)
 CASES = {"cfg2": (2, {}), "cfg2_slippery": (2, {"slippery": 1}), "cfg3": (3, {}), "cfg4": (4, {}), "cfg5": (5, {}),
+         "cfg8": (8, {}),
          # BASELINE's whole cfg 4 (2^19 lanes) on one GPU, as bench.py --config 4 --lanes 524288
          "cfg4_2p19": (4, {"n_lanes": 1 << 19})}
 
@@ -68,9 +69,26 @@ def _arrays(args):
     return out
 
 
+def _drift(q, qs):
+    both = np.isfinite(q) & np.isfinite(qs)
+    d = np.abs(q[both] - qs[both])
+    return {"nan_masks_equal": bool(np.array_equal(np.isnan(q), np.isnan(qs))),
+            "linf": float(d.max()) if d.size else 0.0,
+            "rel_linf": float((d / np.maximum(np.abs(q[both]), 1.0)).max()) if d.size else 0.0}
+
+
 def case(name):
-    with ProcessPoolExecutor(max_workers=2) as ex:
-        a, sq = ex.map(_arrays, [(name, "auto"), (name, "f64_seq")])
+    # fixed-point cases also run the order-free f64 (exact-grid) schedule, so the
+    # drift splits into representation rounding (fixed point vs f64 exact grid,
+    # both order-free) and summation order (f64 exact grid vs f64 sequential):
+    # VERDICT r04 item 8
+    kw0 = __import__("make_fullsize").bench_params(*CASES[name])
+    fixed = kw0["agent"] == "one_step" and kw0["policy"] == "tabular" and not (
+        kw0["selector"] == "ucb" and kw0["algo"] == "expected_sarsa")
+    modes = [(name, "auto"), (name, "f64_seq")] + ([(name, "f64")] if fixed else [])
+    with ProcessPoolExecutor(max_workers=len(modes)) as ex:
+        res = list(ex.map(_arrays, modes))
+    a, sq = res[0], res[1]
     kw = a["kw"]
     q = a["q"]
     fin = np.isfinite(q)
@@ -85,14 +103,13 @@ def case(name):
         out["ucb_n_u64_b64"] = b64(np.asarray(n, "<u8"))
         out["ucb_t"] = int(t)
     # drift measurement: sequential f64 sums (same draws, same mean rule)
-    qs = sq["q"]
-    both = np.isfinite(q) & np.isfinite(qs)
-    d = np.abs(q[both] - qs[both])
-    out["seq_sum_drift"] = {
-        "nan_masks_equal": bool(np.array_equal(np.isnan(q), np.isnan(qs))),
-        "linf": float(d.max()) if d.size else 0.0,
-        "rel_linf": float((d / np.maximum(np.abs(q[both]), 1.0)).max()) if d.size else 0.0,
-    }
+    out["seq_sum_drift"] = _drift(q, sq["q"])
+    if fixed:
+        qf = res[2]["q"]
+        out["repr_drift"] = dict(_drift(q, qf), what="fixed point 2^-40 vs f64 exact-grid sums: both order-free, "
+                                                       "the representation alone")
+        out["order_drift"] = dict(_drift(qf, sq["q"]), what="f64 exact-grid vs f64 sequential sums: the "
+                                                            "summation order alone")
     return name, out
 
 

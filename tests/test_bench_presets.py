@@ -23,6 +23,7 @@ def _parse(monkeypatch, *argv):
     (5, "blackjack", "double", 1 << 19, 512),
     (6, "frozen_lake", "neural", 1 << 20, 1),
     (7, "cliff_walking", "tabular", 1 << 20, 1),
+    (8, "taxi", "tabular", 1 << 20, 512),
 ])
 def test_presets(monkeypatch, cfg, env, policy, lanes, group):
     a = _parse(monkeypatch, "--config", str(cfg))
@@ -34,6 +35,8 @@ def test_presets(monkeypatch, cfg, env, policy, lanes, group):
         assert a.extra["planning"] == 10 and a.agent == "one_step" and a.algo == "qlearning"
     if cfg == 2:
         assert a.map8x8 == 1 and a.extra == {}
+    if cfg == 8:   # cfg 3's Taxi + UCB, Q-learning target: the finite regime
+        assert (a.selector, a.algo) == ("ucb", "qlearning")
 
 
 def test_workload_keys_distinct(monkeypatch):
@@ -41,6 +44,6 @@ def test_workload_keys_distinct(monkeypatch):
     keys = set()
     for argv in (["--config", "2"], ["--config", "2", "--slippery", "1"], ["--config", "2", "--q-mode", "f64"],
                  ["--config", "3"], ["--config", "4"], ["--config", "4", "--lanes", str(1 << 19)],
-                 ["--config", "5"], ["--config", "6"], ["--config", "7"]):
+                 ["--config", "5"], ["--config", "6"], ["--config", "7"], ["--config", "8"]):
         keys.add(bench.workload_key(_parse(monkeypatch, *argv)))
-    assert len(keys) == 9
+    assert len(keys) == 10

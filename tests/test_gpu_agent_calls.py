@@ -265,3 +265,53 @@ def test_batched_call_lengths_and_view_readiness(rl):
     assert ex.value.code == 1               # EnvNotReady until the view resets the lane
     env.reset_lane(0)
     env.step_lane(0, 1)
+
+
+def fused_train(agent, n_episodes, eval_at):
+    """INTEGRATION.md §1.1's `impl Agent for GpuAgent` override of train
+    (src/agent.rs:66-118) on a one-lane handle: ONE rl_agent_train (the fused
+    private kernel) with the episode log and step records on, and the reference's
+    history tuple read back from them"""
+    agent.set_episode_log(2 * n_episodes + 8 * eval_at + 1024)
+    agent.set_recording(True)
+    agent.records()                           # drop older records
+    agent.train(n_episodes, eval_at)
+    eps, lost = agent.episodes()
+    assert lost == 0
+    recs = agent.records()[:, 0]
+    agent.set_recording(False)
+    train = eps[eps["mode"] == 0]
+    td = recs["td"][((recs["kind"] == 2) | (recs["kind"] == 3)) & (recs["mode"] == 0)]
+    return list(train["reward"]), list(train["length"]), list(td)
+
+
+def fused_evaluate(agent, n_episodes):
+    """the override of evaluate (src/agent.rs:120-141): one rl_agent_evaluate"""
+    agent.set_episode_log(n_episodes + 1024)
+    agent.evaluate(n_episodes)
+    eps, lost = agent.episodes()
+    assert lost == 0
+    return list(eps["reward"]), list(eps["length"])
+
+
+@pytest.mark.parametrize("case,n", [CASES[0], CASES[2], CASES[3], CASES[5]],
+                         ids=["fl-q", "cw-traces", "taxi-ucb-es", "bj-double"])
+def test_trait_override_equals_default_body(rl, case, n):
+    """the override of train / evaluate (one fused launch
+    sequence) returns exactly what the trait's default bodies return when they run
+    over the per-call get_action / update: histories, TD stream, Q, epsilon"""
+    p = rl.default_params(n_lanes=1, group_size=1, n_episodes_for_decay=n, **case)
+    a1, a2 = rl.Agent(p), rl.Agent(p)
+    env = a1.env()
+    eval_at = max(n // 3, 1)
+    r1, l1, te1 = reference_train(a1, env, n, eval_at)
+    r2, l2, te2 = fused_train(a2, n, eval_at)
+    _bits_equal(r1, r2)
+    assert l1 == [int(x) for x in l2]
+    _bits_equal(te1, te2)
+    er1, el1 = reference_evaluate(a1, env, 20)
+    er2, el2 = fused_evaluate(a2, 20)
+    _bits_equal(er1, er2)
+    assert el1 == [int(x) for x in el2]
+    _bits_equal(a1.q().reshape(-1), a2.q().reshape(-1))
+    _bits_equal(a1.epsilon(), a2.epsilon())

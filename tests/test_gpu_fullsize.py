@@ -32,7 +32,7 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5", "cfg4_2p19"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5", "cfg4_2p19", "cfg8"])
 def test_bench_config_matches_fullsize_fixture(rl, name):
     import sys
     sys.path.insert(0, os.path.dirname(HERE))

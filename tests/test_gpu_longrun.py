@@ -1,6 +1,6 @@
 """GPU parity over the whole benchmarked window.
 
-bench.py's cfg 2 / 2-slippery / 3 / 4 / 5 presets (2^20 / 2^20 / 2^20 / 2^17 /
+bench.py's cfg 2 / 2-slippery / 3 / 4 / 5 / 8 presets (2^20 / 2^20 / 2^20 / 2^17 /
 2^19 lanes per GPU, groups of 512 / 512 / 512 / 256 / 512, K = 64), and cfg 4 at
 BASELINE's whole 2^19 lanes on one GPU (`bench.py --config 4 --lanes 524288`), run for the
 65 launches one default bench run makes (1 warm-up + 64 timed) and are compared
@@ -33,7 +33,7 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5", "cfg4_2p19"])
+@pytest.mark.parametrize("name", ["cfg2", "cfg2_slippery", "cfg3", "cfg4", "cfg5", "cfg4_2p19", "cfg8"])
 def test_bench_window_matches_oracle(rl, name):
     sys.path.insert(0, HERE)
     from golden.make_fullsize import bench_params
@@ -43,7 +43,7 @@ def test_bench_window_matches_oracle(rl, name):
     assert kw == g["params"], "bench.py presets moved: regenerate tests/golden/longrun.json"
     dev = rl.Agent(rl.default_params(**{k: v for k, v in kw.items() if k != "reset_step"}))
     dev.set_reset_step(bool(kw["reset_step"]))
-    assert dev.q_repr() == g["q_repr"] == ("fixed40" if name.startswith("cfg2") else "f64")
+    assert dev.q_repr() == g["q_repr"] == ("fixed40" if name.startswith("cfg2") or name == "cfg8" else "f64")
     dev.run(g["launches"])
     assert dev.q_repr() == g["q_repr"]
     want = np.frombuffer(base64.b64decode(g["q_raw_i64_b64"]), "<i8")
