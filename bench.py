@@ -417,8 +417,11 @@ def main():
         comm = rccl_bootstrap(rank, world, dev)
         agent.set_comm(comm)                # every merge: RCCL all-reduces over xGMI, then apply
     elif dist_on:
-        agent.set_stream(torch.cuda.current_stream().cuda_stream)
+        # rehearsal: torch's HIP runtime (its wheel's own) and librlamd's are not one
+        # runtime, so their streams do not order each other: every hand-over below is
+        # an explicit synchronize on both sides
         delta = torch.zeros(agent.delta_words(), dtype=torch.int64, device=f"cuda:{dev}")
+        torch.cuda.synchronize()
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
         agent.set_merge_groups(world * ((args.lanes + args.group - 1) // args.group))
     mw = agent.delta_max_words()
@@ -428,9 +431,13 @@ def main():
             agent.run(1)
             return
         agent.launch_train()                # rehearsal: torch all_reduces of the merge buffer
+        agent.synchronize()
         dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
+        torch.cuda.synchronize()
         agent.launch_fold()
+        agent.synchronize()
         dist.all_reduce(delta[mw:])
+        torch.cuda.synchronize()
         agent.launch_apply()
 
     def barrier():

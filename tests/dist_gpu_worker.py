@@ -37,13 +37,15 @@ def main():
     groups = (L + case["group_size"] - 1) // case["group_size"]
     a.set_merge_groups(world * groups)          # the f64 merge grid counts every rank's groups
     repr_rank = a.q_repr()
+    # torch's HIP runtime (its wheel's own) and librlamd's do not order each other's
+    # streams: each hand-over synchronizes the side that wrote the buffer
     for _ in range(n_launch):
         a.launch_train()
-        torch.cuda.synchronize()
+        a.synchronize()
         dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
         torch.cuda.synchronize()
         a.launch_fold()
-        torch.cuda.synchronize()
+        a.synchronize()
         dist.all_reduce(delta[mw:])
         torch.cuda.synchronize()
         a.launch_apply()

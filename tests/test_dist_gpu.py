@@ -93,3 +93,21 @@ def test_bench_rccl_path_one_rank():
     assert len(lines) == 1, r.stdout
     d = lines[0]
     assert d["config"]["collective"].startswith("rccl") and d["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra,fixture,scaling", [([], "cfg2_L2M_25", "weak"),
+                                                    (["--lanes-total", str(1 << 20)], "cfg2_L1M_25", "strong")],
+                         ids=["weak-2x2^20", "strong-2^20"])
+def test_bench_two_ranks_q_check_matches_one_process(extra, fixture, scaling):
+    """a 2-rank bench run in the driver's shape (--steps 20
+    --warmup 5) ends with the merged Q of ONE process over its global lane set:
+    every rank holds the same digest and it equals the oracle's for that set
+    (tests/golden/global_q.json) — weak (2 x 2^20 lanes) and the north star's
+    strong split of 2^20 lanes"""
+    r = _torchrun(["bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu-baseline"] + extra)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    qc = d["q_check"]
+    assert d["scaling"] == scaling and qc["global_lanes"] == (2 << 20 if scaling == "weak" else 1 << 20)
+    assert qc["ranks_agree"] is True and qc["fixture"] == fixture and qc["match"] is True, json.dumps(qc)
