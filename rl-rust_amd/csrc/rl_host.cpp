@@ -491,6 +491,33 @@ int agent_select_kernel(rl_agent *a) {
         a->grid = dim3((a->L + 255) / 256);
         a->smem = private_smem_bytes(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->S,
                                      a->A, (uint32_t)a->eh.cdf.size());
+        // small tables (FrozenLake, CliffWalking; single or double): the launch's
+        // lanes keep their Q in LDS (k_train_private_lds), 4 waves of priv_lpw lanes
+        // per block (8: 32 lanes, 50 KB for CliffWalking, 3 blocks per CU); slots of
+        // P*S*A + 2 f64.  RLAMD_PRIV_LPW = 0 / 2 / 4 / 8 / 16 / 32 / 64 overrides (0: Q in HBM)
+        a->kp.priv_lpw = 0;
+        const int ek = a->cfg.env.kind;
+        // (a NeuralPolicy's parameters in LDS measured 2x SLOWER than its coalesced
+        // HBM stream at 16 lanes per wave — the forward / backward passes are VALU work
+        // that idle lanes waste: cfg 6 219 against 102 ms per launch, so not for it)
+        const uint64_t psa = (uint64_t)a->P * a->S * a->A;
+        uint32_t lpw = (!a->neural && psa * 8 <= 4096 &&
+                        (ek == RL_ENV_FROZEN_LAKE || ek == RL_ENV_CLIFF_WALKING || ek == RL_ENV_FROZEN_LAKE_EDITED))
+                           ? 8u : 0u;
+        if (const char *e = getenv("RLAMD_PRIV_LPW")) {
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v == 0 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64) lpw = lpw ? v : 0u;
+        }
+        if (lpw) {
+            const uint32_t nl = 4u * lpw;
+            const size_t smem = ((a->smem + 15) & ~(size_t)15) + (size_t)nl * (psa + 2) * 8;
+            if (smem <= 160 * 1024) {
+                a->kp.priv_lpw = lpw;
+                a->block = dim3(256);
+                a->grid = dim3((a->L + nl - 1) / nl);
+                a->smem = smem;
+            }
+        }
     } else {
         a->kp.ucb_pack = (uint64_t)a->G * a->K < 65536ull ? 1 : 0;   // UCB + expected SARSA counters (KParams)
         const uint32_t g = std::min(a->G, a->L);

@@ -158,6 +158,9 @@ struct KParams {
     // the other wave slots idle
     uint32_t lpw;
     uint32_t trc_kb;       // LDS KiB per learner group for pair-trace slots (rl_train_impl.h smem_layout)
+    // private mode with small tables (round 5): lanes per wave of k_train_private_lds,
+    // which holds its lanes' Q tables in LDS for the launch (0: k_train_private, Q in HBM)
+    uint32_t priv_lpw;
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

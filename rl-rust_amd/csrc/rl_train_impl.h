@@ -450,6 +450,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_PLAN_PF
+#define RLAMD_PLAN_PF 1   // Dyna planning (eps-greedy): a batch's draws first, its model reads together
+#endif
 #ifndef RLAMD_LAZY_ROWS
 #define RLAMD_LAZY_ROWS 1   // reset-and-step: the reset's selection reads its row only for exploiting lanes
 #endif
@@ -2141,7 +2144,7 @@ constexpr bool use_o8() {
 // ======================================================================== private
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
-                                                 LaneRegs &L, Counters &C);
+                                                 LaneRegs &L, Counters &C, double *qb);
 
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __global__ void __launch_bounds__(256) k_train_private(KParams p) {
@@ -2172,7 +2175,63 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
     LaneRegs L;
     Counters C;
     lane_load(p, lane, active, L);
-    if (active) run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L, C);
+    if (active)
+        run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L, C,
+                                                        p.q_priv ? p.q_priv + lane * (uint64_t)(P * SA) : nullptr);
+    flush_stats(p, L, C, active, ACC);
+}
+
+// Private agents with small tables (KParams::priv_lpw != 0; FrozenLake 4x4 / 8x8,
+// CliffWalking, single or double): the launch's lanes hold their Q tables in LDS.
+// A block is 4 waves of priv_lpw lanes each (the other threads of a wave idle:
+// cfg 7 19.9 ms per launch at 8 lanes per wave, 28.2 at 4, 31.4 at 16, 41.5 with Q
+// in HBM — profiles/r05/private_lds_lpw_sweep.txt, cfg7_private_lds_ab.txt),
+// its lanes' tables — one contiguous run of the lane-major q_priv — are copied in,
+// the K steps read and write only LDS, and the tables go back at the end.  Each
+// lane's slot is padded by two f64, so the slots of a wave's lanes start in
+// different banks.  Private random gathers from HBM cost a 64-byte sector per
+// 8-32 useful bytes (cfg 7: 7.5x the algorithmic traffic in the lane-major HBM form).
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+__global__ void __launch_bounds__(256) k_train_private_lds(KParams p) {
+    using E = EnvDev<ENV>;
+    constexpr int A = E::A;
+    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    constexpr bool UCB = SEL == RL_SEL_UCB;
+    const uint32_t S = p.S, SA = S * (uint32_t)A, PSA = (uint32_t)P * SA, stride = PSA + 2u;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const SmemLayout lay = smem_layout(ENV, P, UCB, AGENT == RL_AGENT_TRACES ? 1 : 0, S, A, p.n_start, 0u);
+    uint32_t *TR = (uint32_t *)(smem + lay.tr);
+    unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
+    double *QS = (double *)(smem + align16(lay.total));
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x, lpw = p.priv_lpw, nl = (nthr >> 6) * lpw;
+    const uint64_t lane0 = (uint64_t)blockIdx.x * nl;
+    const uint32_t nv = lane0 + nl <= p.L ? nl : (uint32_t)(p.L - lane0);   // lanes of this block
+    if (tid < STATS_W) ACC[tid] = 0ull;
+    if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
+        for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
+    const double *qg = p.q_priv + lane0 * PSA;                   // the block's tables, contiguous
+    for (uint32_t l = 0; l < nv; ++l)
+        for (uint32_t e = tid; e < PSA; e += nthr) QS[l * stride + e] = qg[(uint64_t)l * PSA + e];
+    __syncthreads();
+
+    EnvTables tabs;
+    tabs.trans = TR; tabs.cdf = p.start_cdf; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+    tabs.fixed_start = p.fixed_start;
+    tabs.slippery = p.slippery;
+
+    const uint32_t slot = (tid >> 6) * lpw + (tid & 63u);
+    const uint64_t lane = lane0 + slot;
+    const bool active = (tid & 63u) < lpw && slot < nv;
+    LaneRegs L;
+    Counters C;
+    lane_load(p, lane, active, L);
+    if (active) run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L, C, QS + slot * stride);
+    __syncthreads();
+    double *qo = p.q_priv + lane0 * PSA;
+    for (uint32_t l = 0; l < nv; ++l)
+        for (uint32_t e = tid; e < PSA; e += nthr) qo[(uint64_t)l * PSA + e] = QS[l * stride + e];
     flush_stats(p, L, C, active, ACC);
 }
 
@@ -2196,17 +2255,18 @@ struct PrivAgent {
     uint32_t tcnt;     // traces: visited states this episode
     const NetLane net;
     NetCache<A> nc;
+    double *const qb;   // the lane's Q block [P][S][A]: in HBM (q_priv, lane-major) or its LDS slot
 
-    __device__ __forceinline__ PrivAgent(const KParams &p_, uint64_t lane_, LaneRegs &L_, Counters &C_)
+    __device__ __forceinline__ PrivAgent(const KParams &p_, uint64_t lane_, LaneRegs &L_, Counters &C_, double *qb_)
         : p(p_), lane(lane_), Ls(p_.L), SA(p_.S * (uint32_t)A), L(L_), C(C_),
           t(UCB ? p_.t_priv[lane_] : 0), tcnt(AGENT == RL_AGENT_TRACES ? p_.tcnt[lane_] : 0u),
-          net{p_.net_w, p_.L, lane_, p_.n_in, p_.n_hidden, (uint32_t)A} {}
+          net{p_.net_w, p_.L, lane_, p_.n_in, p_.n_hidden, (uint32_t)A}, qb(qb_) {}
     __device__ __forceinline__ void store() {
         if (UCB) p.t_priv[lane] = t;
         if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
     }
     // lane-major tables (rl_kparams.h): the lane's Q block [P][S][A], its UCB counts [S][A]
-    __device__ __forceinline__ double &qref(uint32_t idx) const { return p.q_priv[lane * (uint64_t)(P * SA) + idx]; }
+    __device__ __forceinline__ double &qref(uint32_t idx) const { return qb[idx]; }
     __device__ __forceinline__ uint64_t &nref(uint32_t idx) const { return p.n_priv[lane * (uint64_t)SA + idx]; }
     // row s of table tbl: A consecutive f64, 16-byte aligned (P*S*A and A even for every env)
     __device__ __forceinline__ void row(uint32_t tbl, uint32_t s, double (&v)[A]) const {
@@ -2345,26 +2405,67 @@ struct PrivAgent {
                 ++mc;
                 p.mcnt[lane] = mc;
             }
-            for (uint32_t i = 0; i < p.plan_steps; ++i) {
-                const uint32_t j = gen_index(L.rng, mc);
-                const uint4 m = mrec[j];                         // one 16-byte read
-                const uint32_t pk = m.x;
-                const uint32_t ps2 = m.y;
-                const double pr = __longlong_as_double((long long)(((uint64_t)m.w << 32) | m.z));
-                const uint32_t na = select(ps2);
-                update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
+            if constexpr (!UCB && !NEURAL && RLAMD_PLAN_PF) {
+                // eps-greedy draws depend on the stream and eps only, never on Q: a batch
+                // of planning steps takes its draws first (gen_index, the eps test, the
+                // exploring action: the order of the loop below), issues its model reads
+                // together, then runs the selections and updates in order — the exploit
+                // argmax reads Q after the previous planning updates, as the loop does
+                constexpr uint32_t PB = 8;
+                for (uint32_t i0 = 0; i0 < p.plan_steps; i0 += PB) {
+                    const uint32_t nb = p.plan_steps - i0 < PB ? p.plan_steps - i0 : PB;
+                    uint4 m[PB];
+                    uint32_t acts = 0;                        // 4 bits per step: action + 1, 0 = exploit
+#pragma unroll
+                    for (uint32_t b = 0; b < PB; ++b) {
+                        if (b < nb) {
+                            const uint32_t j = gen_index(L.rng, mc);
+                            uint32_t a1 = 0;
+                            if (L.eps != 0.0 && eps_test(L.rng, L.eps)) a1 = uniform_action<A>(L.rng) + 1u;
+                            acts |= a1 << (4u * b);
+                            m[b] = mrec[j];                    // one 16-byte read each, all in flight
+                        }
+                    }
+#pragma unroll
+                    for (uint32_t b = 0; b < PB; ++b) {
+                        if (b < nb) {
+                            const uint32_t pk = m[b].x, ps2 = m[b].y;
+                            const double pr = __longlong_as_double((long long)(((uint64_t)m[b].w << 32) | m[b].z));
+                            const uint32_t a1 = (acts >> (4u * b)) & 0xfu;
+                            uint32_t na;
+                            if (a1) {
+                                na = a1 - 1u;
+                            } else {
+                                double v[A];
+                                predict(ps2, v);
+                                na = argmax<A>(v);
+                            }
+                            update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
+                        }
+                    }
+                }
+            } else {
+                for (uint32_t i = 0; i < p.plan_steps; ++i) {
+                    const uint32_t j = gen_index(L.rng, mc);
+                    const uint4 m = mrec[j];                         // one 16-byte read
+                    const uint32_t pk = m.x;
+                    const uint32_t ps2 = m.y;
+                    const double pr = __longlong_as_double((long long)(((uint64_t)m.w << 32) | m.z));
+                    const uint32_t na = select(ps2);
+                    update(pk / (uint32_t)A, pk % (uint32_t)A, pr, false, ps2, na);
+                }
             }
         }
         return td;
     }
 };
 
-// one private lane (a whole reference agent) for K synchronous steps
+// one private lane (a whole reference agent) for K synchronous steps, its Q at qb
 template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
-                                                 LaneRegs &L, Counters &C) {
+                                                 LaneRegs &L, Counters &C, double *qb) {
     using E = EnvDev<ENV>;
-    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C);
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C, qb);
     for (uint32_t k = 0; k < p.K; ++k) {
         if (L.mode == RL_MODE_DONE) {
             if (p.rec) write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
@@ -2424,7 +2525,9 @@ __global__ void __launch_bounds__(256) k_agent_call(KParams p) {
     LaneRegs L;
     Counters C;
     lane_load(p, lane, true, L);
-    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C);
+    constexpr int P = POLICY == RL_POLICY_DOUBLE ? 2 : 1;
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C,
+                                               p.q_priv ? p.q_priv + lane * (uint64_t)(P * p.S * EnvDev<ENV>::A) : nullptr);
     const AgentCall &c = p.call;
     if (p.call_op == CALL_GET_ACTION) {
         c.action_out[i] = ag.select(c.s[i]);
@@ -2448,6 +2551,8 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
                                    dim3((p.call_n + 255) / 256), dim3(256), args, 0, stream);
         }
         k = (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>;
+        if constexpr (POLICY != RL_POLICY_NEURAL && ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
+            if (p.priv_lpw) k = (const void *)k_train_private_lds<ENV, AGENT, POLICY, SEL, ALGO>;
     } else if (instr) {
         k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, true>(p);
     } else {
