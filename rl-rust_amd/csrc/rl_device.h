@@ -370,29 +370,58 @@ __device__ inline double rl_tanh(double x) {
 __device__ __forceinline__ double max_rs(double a, double b) { return (a > b || b != b) ? a : b; }
 __device__ __forceinline__ double min_rs(double a, double b) { return (a < b || b != b) ? a : b; }
 __device__ __forceinline__ double sigmoid_(double v) { return 1.0 / (1.0 + rl_exp(-v)); }
+// act_t / act_pt: one activation as a compile-time choice (the register-resident
+// network kernel, rl_net.h NetRegs); act_f / act_fp: the run-time switch over them
+template <int ACT>
+__device__ __forceinline__ double act_t(double v) {
+    if constexpr (ACT == RL_ACT_TANH) return rl_tanh(v);
+    else if constexpr (ACT == RL_ACT_RELU) return max_rs(v, 0.0);
+    else if constexpr (ACT == RL_ACT_LEAKY_RELU) return max_rs(v, 0.1 * v);
+    else if constexpr (ACT == RL_ACT_RELU6) return min_rs(max_rs(v, 0.0), 6.0);
+    // v and 0.1 v share a sign (and are both NaN or neither), so max_rs is the
+    // hardware max here, and min_rs against 6.0 the hardware min: the same value
+    // (NaN payloads aside) in 2 instructions instead of 6
+    else if constexpr (ACT == RL_ACT_LEAKY_RELU6) return __builtin_fmin(__builtin_fmax(v, 0.1 * v), 6.0);
+    else if constexpr (ACT == RL_ACT_SIGMOID) return sigmoid_(v);
+    else if constexpr (ACT == RL_ACT_SWISH) return v * sigmoid_(v);
+    else if constexpr (ACT == RL_ACT_HARD_SWISH) return (v * min_rs(max_rs(v + 3.0, 0.0), 6.0)) / 6.0;
+    else return v;
+}
+template <int ACT>
+__device__ __forceinline__ double act_pt(double v) {
+    if constexpr (ACT == RL_ACT_TANH) { const double t = rl_tanh(v); return 1.0 - t * t; }
+    else if constexpr (ACT == RL_ACT_RELU) return v > 0.0 ? 1.0 : 0.0;
+    else if constexpr (ACT == RL_ACT_LEAKY_RELU) return v > 0.0 ? 1.0 : 0.01;
+    else if constexpr (ACT == RL_ACT_RELU6) return (v > 0.0 && v < 6.0) ? 1.0 : 0.0;
+    else if constexpr (ACT == RL_ACT_LEAKY_RELU6) return (v > 0.0 && v < 6.0) ? 1.0 : 0.01;
+    else if constexpr (ACT == RL_ACT_SIGMOID) { const double sg = sigmoid_(v); return sg * (1.0 - sg); }
+    else if constexpr (ACT == RL_ACT_SWISH) { const double e = rl_exp(v); return (e * (v + e + 1.0)) / ((e + 1.0) * (e + 1.0)); }
+    else if constexpr (ACT == RL_ACT_HARD_SWISH) return v > -3.0 ? (2.0 * v + 3.0) / 6.0 : 0.0;
+    else return 1.0;
+}
 __device__ inline double act_f(int act, double v) {
     switch (act) {
-    case RL_ACT_TANH: return rl_tanh(v);
-    case RL_ACT_RELU: return max_rs(v, 0.0);
-    case RL_ACT_LEAKY_RELU: return max_rs(v, 0.1 * v);
-    case RL_ACT_RELU6: return min_rs(max_rs(v, 0.0), 6.0);
-    case RL_ACT_LEAKY_RELU6: return min_rs(max_rs(v, 0.1 * v), 6.0);
-    case RL_ACT_SIGMOID: return sigmoid_(v);
-    case RL_ACT_SWISH: return v * sigmoid_(v);
-    case RL_ACT_HARD_SWISH: return (v * min_rs(max_rs(v + 3.0, 0.0), 6.0)) / 6.0;
+    case RL_ACT_TANH: return act_t<RL_ACT_TANH>(v);
+    case RL_ACT_RELU: return act_t<RL_ACT_RELU>(v);
+    case RL_ACT_LEAKY_RELU: return act_t<RL_ACT_LEAKY_RELU>(v);
+    case RL_ACT_RELU6: return act_t<RL_ACT_RELU6>(v);
+    case RL_ACT_LEAKY_RELU6: return act_t<RL_ACT_LEAKY_RELU6>(v);
+    case RL_ACT_SIGMOID: return act_t<RL_ACT_SIGMOID>(v);
+    case RL_ACT_SWISH: return act_t<RL_ACT_SWISH>(v);
+    case RL_ACT_HARD_SWISH: return act_t<RL_ACT_HARD_SWISH>(v);
     default: return v;
     }
 }
 __device__ inline double act_fp(int act, double v) {
     switch (act) {
-    case RL_ACT_TANH: { const double t = rl_tanh(v); return 1.0 - t * t; }
-    case RL_ACT_RELU: return v > 0.0 ? 1.0 : 0.0;
-    case RL_ACT_LEAKY_RELU: return v > 0.0 ? 1.0 : 0.01;
-    case RL_ACT_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.0;
-    case RL_ACT_LEAKY_RELU6: return (v > 0.0 && v < 6.0) ? 1.0 : 0.01;
-    case RL_ACT_SIGMOID: { const double sg = sigmoid_(v); return sg * (1.0 - sg); }
-    case RL_ACT_SWISH: { const double e = rl_exp(v); return (e * (v + e + 1.0)) / ((e + 1.0) * (e + 1.0)); }
-    case RL_ACT_HARD_SWISH: return v > -3.0 ? (2.0 * v + 3.0) / 6.0 : 0.0;
+    case RL_ACT_TANH: return act_pt<RL_ACT_TANH>(v);
+    case RL_ACT_RELU: return act_pt<RL_ACT_RELU>(v);
+    case RL_ACT_LEAKY_RELU: return act_pt<RL_ACT_LEAKY_RELU>(v);
+    case RL_ACT_RELU6: return act_pt<RL_ACT_RELU6>(v);
+    case RL_ACT_LEAKY_RELU6: return act_pt<RL_ACT_LEAKY_RELU6>(v);
+    case RL_ACT_SIGMOID: return act_pt<RL_ACT_SIGMOID>(v);
+    case RL_ACT_SWISH: return act_pt<RL_ACT_SWISH>(v);
+    case RL_ACT_HARD_SWISH: return act_pt<RL_ACT_HARD_SWISH>(v);
     default: return 1.0;
     }
 }

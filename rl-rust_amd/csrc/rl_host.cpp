@@ -508,12 +508,27 @@ int agent_select_kernel(rl_agent *a) {
             const uint32_t v = (uint32_t)atoi(e);
             if (v == 0 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64) lpw = lpw ? v : 0u;
         }
+        // the bin's network (frozen_lake_neural.rs:130-134) on one-step agents: the
+        // lane's parameters in registers for the launch (k_train_private_net);
+        // RLAMD_NET_REGS=0 keeps them in HBM (experiments)
+        a->kp.net_regs = 0;
+        if (a->neural && a->cfg.agent == RL_AGENT_ONE_STEP && a->A == 4 && a->n_in == 1 &&
+            a->cfg.net.hidden == 32 && a->cfg.net.act_hidden == RL_ACT_LEAKY_RELU6 &&
+            a->cfg.net.act_out == RL_ACT_LINEAR && ek == RL_ENV_FROZEN_LAKE) {
+            const char *e = getenv("RLAMD_NET_REGS");
+            a->kp.net_regs = (e && atoi(e) == 0) ? 0u : 1u;
+        }
+        uint32_t pwv = 4;   // waves per block (RLAMD_PRIV_WAVES = 1 / 2 / 4: experiments)
+        if (const char *e = getenv("RLAMD_PRIV_WAVES")) {
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v == 1 || v == 2 || v == 4) pwv = v;
+        }
         if (lpw) {
-            const uint32_t nl = 4u * lpw;
+            const uint32_t nl = pwv * lpw;
             const size_t smem = ((a->smem + 15) & ~(size_t)15) + (size_t)nl * (psa + 2) * 8;
             if (smem <= 160 * 1024) {
                 a->kp.priv_lpw = lpw;
-                a->block = dim3(256);
+                a->block = dim3(64 * pwv);
                 a->grid = dim3((a->L + nl - 1) / nl);
                 a->smem = smem;
             }

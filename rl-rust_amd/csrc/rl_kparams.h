@@ -161,6 +161,7 @@ struct KParams {
     // private mode with small tables (round 5): lanes per wave of k_train_private_lds,
     // which holds its lanes' Q tables in LDS for the launch (0: k_train_private, Q in HBM)
     uint32_t priv_lpw;
+    uint32_t net_regs;     // 1: NeuralPolicy lanes of the bin's network run k_train_private_net (rl_train_impl.h)
 };
 
 // one entry per (env, agent, policy, selector, private) kernel instantiation

@@ -2142,7 +2142,7 @@ constexpr bool use_o8() {
 }
 
 // ======================================================================== private
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
                                                  LaneRegs &L, Counters &C, double *qb);
 
@@ -2179,6 +2179,61 @@ __global__ void __launch_bounds__(256) k_train_private(KParams p) {
         run_private_lane<ENV, AGENT, POLICY, SEL, ALGO>(p, tabs, lane, L, C,
                                                         p.q_priv ? p.q_priv + lane * (uint64_t)(P * SA) : nullptr);
     flush_stats(p, L, C, active, ACC);
+}
+
+// NeuralPolicy lanes with the bin's network (frozen_lake_neural.rs:130-134:
+// DenseLayer(1, 32) -> leaky_relu6 -> DenseLayer(32, 4) -> linear on FrozenLake's
+// scalar observation, one-step agents):
+// each thread holds its lane's 196 f64 parameters in registers for the launch
+// (one wave per SIMD: the 392 parameter registers and the step's temporaries fit
+// the 512 of a lane at that occupancy), loaded once from the [param][lane] HBM
+// layout and written back once.  k_train_private with NetLane reads the
+// parameters three times per step and writes them once (6.3 KB per env-step,
+// 421 GB per cfg 6 launch at 0.52 of HBM peak); here the step loop touches no
+// parameter memory.  Same operations in the same order: bit-identical.
+#ifndef RLAMD_NET_PAIR
+#define RLAMD_NET_PAIR 1   // NeuralPolicy: the step's two predicts in one parameter pass
+#endif
+#ifndef RLAMD_NET_REGS
+#define RLAMD_NET_REGS 1
+#endif
+template <int ENV, int AGENT, int SEL, int ALGO>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_train_private_net(KParams p) {
+    using E = EnvDev<ENV>;
+    constexpr int A = E::A;
+    constexpr bool UCB = SEL == RL_SEL_UCB;
+    const uint32_t S = p.S, SA = S * (uint32_t)A;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const SmemLayout lay = smem_layout(ENV, 1, UCB, 0, S, A, p.n_start, 0u);
+    uint32_t *TR = (uint32_t *)(smem + lay.tr);
+    unsigned long long *ACC = (unsigned long long *)(smem + lay.st);
+    const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+    if (tid < STATS_W) ACC[tid] = 0ull;
+    if constexpr (ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
+        for (uint32_t i = tid; i < SA; i += nthr) TR[i] = p.trans[i];
+    __syncthreads();
+
+    EnvTables tabs;
+    tabs.trans = TR; tabs.cdf = p.start_cdf; tabs.n_start = p.n_start; tabs.max_steps = p.max_steps;
+    tabs.th1 = p.th1; tabs.th2 = p.th2; tabs.th3 = p.th3; tabs.trunc_reward = p.trunc_reward;
+    tabs.fixed_start = p.fixed_start;
+    tabs.slippery = p.slippery;
+
+    const uint64_t lane = (uint64_t)blockIdx.x * nthr + tid;
+    const bool active = lane < p.L;
+    LaneRegs L;
+    Counters C;
+    lane_load(p, lane, active, L);
+    if (active)
+        run_private_lane<ENV, AGENT, RL_POLICY_NEURAL, SEL, ALGO, NetBin<(uint32_t)A>>(p, tabs, lane, L, C, nullptr);
+    flush_stats(p, L, C, active, ACC);
+}
+// the register-resident network kernel exists for these instantiations; the host
+// (and launch_train) also require the bin's shape and activations at run time
+template <int ENV, int AGENT, int POLICY>
+__host__ __device__ constexpr bool use_net_regs() {
+    return RLAMD_NET_REGS && POLICY == RL_POLICY_NEURAL && AGENT == RL_AGENT_ONE_STEP && ENV == RL_ENV_FROZEN_LAKE;
 }
 
 // Private agents with small tables (KParams::priv_lpw != 0; FrozenLake 4x4 / 8x8,
@@ -2239,7 +2294,7 @@ __global__ void __launch_bounds__(256) k_train_private_lds(KParams p) {
 // over the lane's f64 Q / UCB counters / trace set / network in HBM.  Used by the
 // private training kernel (K steps per launch) and by the per-call Agent surface
 // (k_agent_call: rl_agent_get_action / rl_agent_update).
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane>
 struct PrivAgent {
     using E = EnvDev<ENV>;
     static constexpr int A = E::A;
@@ -2253,17 +2308,19 @@ struct PrivAgent {
     Counters &C;
     uint64_t t;        // UCB t (upper_confidence_bound.rs:13)
     uint32_t tcnt;     // traces: visited states this episode
-    const NetLane net;
+    NET net;           // the network's parameters (NeuralPolicy): HBM (NetLane) or registers (NetRegs)
     NetCache<A> nc;
+    NetCache<A> nc_b;  // the second entry of a paired predict (prefetch_pair)
     double *const qb;   // the lane's Q block [P][S][A]: in HBM (q_priv, lane-major) or its LDS slot
 
     __device__ __forceinline__ PrivAgent(const KParams &p_, uint64_t lane_, LaneRegs &L_, Counters &C_, double *qb_)
         : p(p_), lane(lane_), Ls(p_.L), SA(p_.S * (uint32_t)A), L(L_), C(C_),
           t(UCB ? p_.t_priv[lane_] : 0), tcnt(AGENT == RL_AGENT_TRACES ? p_.tcnt[lane_] : 0u),
-          net{p_.net_w, p_.L, lane_, p_.n_in, p_.n_hidden, (uint32_t)A}, qb(qb_) {}
+          net(NET::template make<A>(p_, lane_)), qb(qb_) {}
     __device__ __forceinline__ void store() {
         if (UCB) p.t_priv[lane] = t;
         if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
+        if constexpr (NEURAL) net.store(p, lane);
     }
     // lane-major tables (rl_kparams.h): the lane's Q block [P][S][A], its UCB counts [S][A]
     __device__ __forceinline__ double &qref(uint32_t idx) const { return qb[idx]; }
@@ -2286,6 +2343,7 @@ struct PrivAgent {
     // Policy::predict (tabular_policy.rs:27-29, double_tabular_policy.rs:31-40, neural_policy.rs:43-47)
     __device__ __forceinline__ void predict(uint32_t s, double (&v)[A]) {
         if constexpr (NEURAL) {
+            if constexpr (RLAMD_NET_PAIR) nc.take(nc_b, s);
             nc.get(p, net, s);
 #pragma unroll
             for (int i = 0; i < A; ++i) v[i] = nc.y[i];
@@ -2310,11 +2368,19 @@ struct PrivAgent {
     // Policy::update with x = td (one-step) or td * E[o][b] (traces)
     __device__ __forceinline__ void pol_update(uint32_t tbl, uint32_t s, uint32_t a, double x) {
         if constexpr (NEURAL) {
+            if constexpr (RLAMD_NET_PAIR) nc.take(nc_b, s);
             net_policy_update<A>(p, net, nc, s, a, x);
+            nc_b.invalidate();                                  // the parameters changed
         } else {
             double &q = qref(tbl * SA + s * A + a);             // tabular_policy.rs:36
             q = q + p.lr * x;
         }
+    }
+    // NeuralPolicy training step: the step's two predicts — get_action(s2) and
+    // update's get_values(s) — in one pass over the parameters (the same values:
+    // nothing changes the parameters between them)
+    __device__ __forceinline__ void prefetch_pair(uint32_t s2, uint32_t s) {
+        if constexpr (NEURAL && RLAMD_NET_PAIR) nc.get_pair(p, net, s2, nc_b, s);
     }
     // Agent::get_action (one_step_agent.rs:48-51) with the reference's immediate UCB increments
     __device__ __forceinline__ uint32_t select(uint32_t s) {
@@ -2461,11 +2527,11 @@ struct PrivAgent {
 };
 
 // one private lane (a whole reference agent) for K synchronous steps, its Q at qb
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
                                                  LaneRegs &L, Counters &C, double *qb) {
     using E = EnvDev<ENV>;
-    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO> ag(p, lane, L, C, qb);
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO, NET> ag(p, lane, L, C, qb);
     for (uint32_t k = 0; k < p.K; ++k) {
         if (L.mode == RL_MODE_DONE) {
             if (p.rec) write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
@@ -2490,6 +2556,8 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             E::step(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
+        if constexpr (POLICY == RL_POLICY_NEURAL && AGENT == RL_AGENT_ONE_STEP)
+            if (L.mode == RL_MODE_TRAIN) ag.prefetch_pair(s2, L.s);
         const uint32_t a2 = ag.select(s2);
         double td = 0.0;
         if (L.mode == RL_MODE_TRAIN) {
@@ -2553,6 +2621,8 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
         k = (const void *)k_train_private<ENV, AGENT, POLICY, SEL, ALGO>;
         if constexpr (POLICY != RL_POLICY_NEURAL && ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
             if (p.priv_lpw) k = (const void *)k_train_private_lds<ENV, AGENT, POLICY, SEL, ALGO>;
+        if constexpr (use_net_regs<ENV, AGENT, POLICY>())
+            if (p.net_regs) k = (const void *)k_train_private_net<ENV, AGENT, SEL, ALGO>;
     } else if (instr) {
         k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, true>(p);
     } else {

@@ -554,6 +554,41 @@ def test_neural_policy_matches_oracle(rl, oracle, case):
     assert ((dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))).all()
 
 
+NET_BIN_CASES = [
+    # the bin's network (1-32-4 leaky_relu6 / linear) on one-step agents: the
+    # register-resident kernel (k_train_private_net); 300 lanes = a partial block
+    dict(env="frozen_lake", algo="qlearning"),
+    dict(env="frozen_lake", algo="sarsa", selector="ucb"),
+    dict(env="frozen_lake", map8x8=1, slippery=1, algo="expected_sarsa"),
+    dict(env="frozen_lake", algo="qlearning", planning=2),
+]
+
+
+@pytest.mark.parametrize("case", NET_BIN_CASES, ids=lambda c: "-".join(f"{v}" for v in c.values()))
+def test_neural_bin_shape_register_kernel(rl, oracle, case):
+    """The bin's network with its parameters held in registers for a launch:
+    episodic train and throughput run, every lane's parameters, Q values, eps and
+    stats bit-exact vs the oracle (NaN-aware: payloads differ between gfx950 and x86)."""
+    kw = dict(case)
+    plan = kw.pop("planning", 0)
+    p = _params(rl, policy="neural", n_lanes=300, group_size=1, sync_every=24, n_episodes_for_decay=40,
+                net_hidden=32, net_act1="leaky_relu6", net_act2="linear", max_steps=30, **kw)
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    if plan:
+        dev.set_planning(plan)
+        ref.set_planning(plan)
+    dev.train(12, 5)
+    ref.train_episodes(12, 5)
+    dev.run(3)
+    ref.run(3)
+    dw, rw = dev.weights(), ref.weights()
+    assert ((dw.view(np.uint64) == rw.view(np.uint64)) | (np.isnan(dw) & np.isnan(rw))).all()
+    _assert_q_equal(dev.q(), ref.q())
+    assert np.array_equal(dev.epsilon().view(np.uint64), ref.lane_eps().view(np.uint64))
+    _assert_stats_equal(dev, ref)
+
+
 def test_neural_weights_roundtrip_and_dyna(rl, oracle):
     """set_weights (Layer::set_weights) then training stays in lockstep; Dyna
     planning over a neural policy (InternalModelAgent) matches too."""
