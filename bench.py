@@ -287,29 +287,51 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     rows = 484 if (args.env == "blackjack" and args.selector != "ucb") else agent.S   # LDS rows per group
     slot_bytes = 8 * agent.P * rows * agent.A * groups if agent.q_repr() == "f64" else 0
     fused_bytes = 2 * 56 * lanes + slot_bytes
+    kname = "k_train_private" if args.group == 1 else "k_train_shared"
+    basis_priv = ("private agents: 2 x 56 B lane record per lane per launch + per env-step the lane's own "
+                  "table traffic (tabular: row s2, Q(s,a) read + written, x (1 + planning steps); neural: "
+                  "weights read by two predicts and read + written by the fit)")
     if args.group == 1:
-        # private agents (one agent per lane, its tables / weights in HBM): per
-        # env-step the TD reads row s2 and Q(s, a) and writes Q(s, a) (tabular,
-        # + the same per Dyna planning step), or reads the weights for the two
-        # predicts and reads + writes them in the fit (NeuralPolicy)
+        # private agents: which kernel the library launches (rl_host.cpp
+        # agent_select_kernel): the bin's network on FrozenLake one-step agents holds
+        # its parameters in registers (k_train_private_net), small tables hold Q in
+        # LDS (k_train_private_lds) — each moves its parameters / tables once in and
+        # once out per launch; otherwise per env-step the TD reads row s2 and Q(s, a)
+        # and writes Q(s, a) (tabular, + the same per Dyna planning step), or the two
+        # predicts read the weights and the fit reads + writes them (NeuralPolicy)
+        planning = args.extra.get("planning", 0)
+        psa8 = 8 * agent.P * agent.S * agent.A
         if args.policy == "neural":
-            per_step = 4 * 8 * agent.net_dims()[2]
+            n_in, hid, npar = agent.net_dims()
+            if (args.env == "frozen_lake" and args.agent == "one_step" and n_in == 1 and hid == 32
+                    and args.extra.get("net_act1", "leaky_relu6") == "leaky_relu6"
+                    and args.extra.get("net_act2", "linear") == "linear"):
+                kname = "k_train_private_net"
+                fused_bytes = 2 * 56 * lanes + 2 * 8 * npar * lanes
+                basis_priv = ("k_train_private_net: 2 x 56 B lane record + the lane's parameters read once and "
+                              "written once per launch (held in registers for the K steps)")
+            else:
+                fused_bytes = 2 * 56 * lanes + 4 * 8 * npar * steps_done / args.steps
+        elif args.env in ("frozen_lake", "cliff_walking", "frozen_lake_edited") and psa8 <= 4096:
+            kname = "k_train_private_lds"
+            # + one 16-byte model record per Dyna planning step
+            fused_bytes = 2 * 56 * lanes + 2 * psa8 * lanes + 16 * planning * steps_done / args.steps
+            basis_priv = ("k_train_private_lds: 2 x 56 B lane record + the lane's Q table read once and written "
+                          "once per launch (held in LDS for the K steps) + a 16 B model record per Dyna "
+                          "planning step")
         else:
-            per_step = 8 * (n_act + 2) * (1 + args.extra.get("planning", 0))
-        fused_bytes = 2 * 56 * lanes + per_step * steps_done / args.steps
+            per_step = 8 * (n_act + 2) * (1 + planning)
+            fused_bytes = 2 * 56 * lanes + per_step * steps_done / args.steps
     fused_frac = fused_bytes / avg_kern_s / HBM_PEAK
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     traffic_frac = (traffic / avg_kern_s / HBM_PEAK) if traffic else None
     pipe = pmc.get("valu_pipe_frac") if pmc else None
     wait = (pmc.get("wave_cycle_split") or {}).get("SQ_WAIT_ANY") if pmc else None
-    out = {"kernel": "k_train_private" if args.group == 1 else "k_train_shared", "kernel_avg_ms": avg_kern_s * 1e3,
+    out = {"kernel": kname, "kernel_avg_ms": avg_kern_s * 1e3,
            "hbm": {"fused_bytes_per_launch": fused_bytes, "fused_frac": fused_frac,
                    "fused_basis": ("2 x 56 B lane record per lane per launch (+ 8 B x LDS entries per group "
                                    "for f64 tables): the fused kernel keeps lanes in registers for K steps")
-                   if args.group != 1 else
-                   ("private agents: 2 x 56 B lane record per lane per launch + per env-step the lane's own "
-                    "table traffic (tabular: row s2, Q(s,a) read + written, x (1 + planning steps); neural: "
-                    "weights read by two predicts and read + written by the fit)"),
+                   if args.group != 1 else basis_priv,
                    "traffic_bytes_per_launch": traffic, "traffic_frac": traffic_frac,
                    "peak_GBps": HBM_PEAK / 1e9},
            "hbm_priced": {"bytes_per_env_step": bytes_per_step, "GBps_equiv": priced / 1e9,
