@@ -1520,7 +1520,10 @@ int rl_agent_set_action_selector(rl_agent *a, int32_t sel, double eps0, double e
 int rl_agent_reset(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
-    if (a->mcnt) HIPC(hipMemsetAsync(a->mcnt, 0, (size_t)a->L * 4, a->stream));   // model.reset
+    if (a->mcnt) {   // model.reset: no entries, no slots (mslot = index + 1, 0 = absent)
+        HIPC(hipMemsetAsync(a->mcnt, 0, (size_t)a->L * 4, a->stream));
+        HIPC(hipMemsetAsync(a->mslot, 0, (size_t)a->S * a->A * a->L * 4, a->stream));
+    }
     int rc = agent_reset_policy(a);
     if (rc) return rc;
     return agent_reset_selector(a);

@@ -102,7 +102,7 @@ struct KParams {
     uint32_t plan_steps;
     uint32_t *mcnt;        // [L]
     uint4 *mrec;           // [L][S*A] entry j of a lane's model: {key = s*A+a, s', r lo, r hi} (16 B)
-    uint32_t *mslot;       // [L][S*A] slot of key (valid iff < mcnt and mrec[slot].x == key)
+    uint32_t *mslot;       // [L][S*A] index + 1 of key in mrec, 0 = absent (cleared when the model empties)
     // NeuralPolicy (private mode): per-lane 2-layer MLP, parameters SoA [param][lane]
     // in the order [W1 n_in x H][b1 H][W2 H x A][b2 A] (rl.h rl_agent_net_dims)
     double *net_w;         // [n_params][L]

@@ -450,6 +450,9 @@ __device__ __forceinline__ void trace_sweep(const KParams &p, uint64_t lane, uin
 // Slots j < cap live in LDS (TRI ids / TRE values, column = thread) for the
 // launch and are found by a scan; slots j >= cap live in HBM (tlist / trace
 // [j][L]) with slot_of [id][L] and the visited-state bitmap vbits for them.
+#ifndef RLAMD_PLAN_PB
+#define RLAMD_PLAN_PB 16   // Dyna planning steps whose draws and model reads go out together
+#endif
 #ifndef RLAMD_PLAN_PF
 #define RLAMD_PLAN_PF 1   // Dyna planning (eps-greedy): a batch's draws first, its model reads together
 #endif
@@ -2311,16 +2314,29 @@ struct PrivAgent {
     NET net;           // the network's parameters (NeuralPolicy): HBM (NetLane) or registers (NetRegs)
     NetCache<A> nc;
     NetCache<A> nc_b;  // the second entry of a paired predict (prefetch_pair)
-    double *const qb;   // the lane's Q block [P][S][A]: in HBM (q_priv, lane-major) or its LDS slot
+    double *const qb;
+    // Dyna (InternalModelAgent): the model's entry count for the launch, and the
+    // slot word of the step's (s, a) read ahead of the step (model_prefetch)
+    uint32_t mc = 0, jpf = 0;
+    bool jpf_ok = false;   // the lane's Q block [P][S][A]: in HBM (q_priv, lane-major) or its LDS slot
 
     __device__ __forceinline__ PrivAgent(const KParams &p_, uint64_t lane_, LaneRegs &L_, Counters &C_, double *qb_)
         : p(p_), lane(lane_), Ls(p_.L), SA(p_.S * (uint32_t)A), L(L_), C(C_),
           t(UCB ? p_.t_priv[lane_] : 0), tcnt(AGENT == RL_AGENT_TRACES ? p_.tcnt[lane_] : 0u),
-          net(NET::template make<A>(p_, lane_)), qb(qb_) {}
+          net(NET::template make<A>(p_, lane_)), qb(qb_) {
+        if (p.plan_steps) mc = p.mcnt[lane];
+    }
     __device__ __forceinline__ void store() {
         if (UCB) p.t_priv[lane] = t;
         if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
         if constexpr (NEURAL) net.store(p, lane);
+        if (p.plan_steps) p.mcnt[lane] = mc;
+    }
+    // the model slot of (s, a), read at the start of a training step so its HBM
+    // round trip overlaps the env step, the selection and the update
+    __device__ __forceinline__ void model_prefetch(uint32_t s, uint32_t a) {
+        jpf = p.mslot[lane * (uint64_t)SA + s * A + a];
+        jpf_ok = true;
     }
     // lane-major tables (rl_kparams.h): the lane's Q block [P][S][A], its UCB counts [S][A]
     __device__ __forceinline__ double &qref(uint32_t idx) const { return qb[idx]; }
@@ -2459,17 +2475,18 @@ struct PrivAgent {
                                                    uint32_t a2) {
         const double td = update(s, a, r, term, s2, a2);
         if (p.plan_steps) {
-            uint32_t mc = p.mcnt[lane];
             const uint32_t key = s * A + a;
             uint4 *const mrec = p.mrec + lane * (uint64_t)SA;     // the lane's model, lane-major
             uint32_t *const mslot = p.mslot + lane * (uint64_t)SA;
-            const uint32_t j0 = mslot[key];
-            if (!(j0 < mc && mrec[j0].x == key)) {
+            // mslot[key] = the entry's index + 1, 0 = not in the model (the host clears
+            // the words when it empties the model)
+            const uint32_t j0 = jpf_ok ? jpf : mslot[key];
+            jpf_ok = false;
+            if (j0 == 0u) {
                 const uint64_t rb = (uint64_t)__double_as_longlong(r);
                 mrec[mc] = make_uint4(key, s2, (uint32_t)rb, (uint32_t)(rb >> 32));
-                mslot[key] = mc;
+                mslot[key] = mc + 1u;
                 ++mc;
-                p.mcnt[lane] = mc;
             }
             if constexpr (!UCB && !NEURAL && RLAMD_PLAN_PF) {
                 // eps-greedy draws depend on the stream and eps only, never on Q: a batch
@@ -2477,18 +2494,20 @@ struct PrivAgent {
                 // exploring action: the order of the loop below), issues its model reads
                 // together, then runs the selections and updates in order — the exploit
                 // argmax reads Q after the previous planning updates, as the loop does
-                constexpr uint32_t PB = 8;
+                // RLAMD_PLAN_PB steps per batch (cfg 7, 10 planning steps: 4 -> 20.28 ms per
+                // launch, 8 -> 19.70, 16 -> 18.99, profiles/r05/cfg7_plan_batch.txt)
+                constexpr uint32_t PB = RLAMD_PLAN_PB;
                 for (uint32_t i0 = 0; i0 < p.plan_steps; i0 += PB) {
                     const uint32_t nb = p.plan_steps - i0 < PB ? p.plan_steps - i0 : PB;
                     uint4 m[PB];
-                    uint32_t acts = 0;                        // 4 bits per step: action + 1, 0 = exploit
+                    std::conditional_t<(PB > 8), uint64_t, uint32_t> acts = 0;                        // 4 bits per step: action + 1, 0 = exploit
 #pragma unroll
                     for (uint32_t b = 0; b < PB; ++b) {
                         if (b < nb) {
                             const uint32_t j = gen_index(L.rng, mc);
                             uint32_t a1 = 0;
                             if (L.eps != 0.0 && eps_test(L.rng, L.eps)) a1 = uniform_action<A>(L.rng) + 1u;
-                            acts |= a1 << (4u * b);
+                            acts |= (decltype(acts))a1 << (4u * b);
                             m[b] = mrec[j];                    // one 16-byte read each, all in flight
                         }
                     }
@@ -2497,7 +2516,7 @@ struct PrivAgent {
                         if (b < nb) {
                             const uint32_t pk = m[b].x, ps2 = m[b].y;
                             const double pr = __longlong_as_double((long long)(((uint64_t)m[b].w << 32) | m[b].z));
-                            const uint32_t a1 = (acts >> (4u * b)) & 0xfu;
+                            const uint32_t a1 = (uint32_t)(acts >> (4u * b)) & 0xfu;
                             uint32_t na;
                             if (a1) {
                                 na = a1 - 1u;
@@ -2548,6 +2567,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             continue;
         }
         const uint32_t mode_before = L.mode;      // STEP: src/agent.rs:88-101
+        if (p.plan_steps && L.mode == RL_MODE_TRAIN) ag.model_prefetch(L.s, L.a);
         uint32_t s2 = 0;
         double r = 0.0;
         bool term = false;
