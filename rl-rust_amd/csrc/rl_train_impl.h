@@ -2145,7 +2145,7 @@ constexpr bool use_o8() {
 }
 
 // ======================================================================== private
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane, bool PLAN = true>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
                                                  LaneRegs &L, Counters &C, double *qb);
 
@@ -2229,7 +2229,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     Counters C;
     lane_load(p, lane, active, L);
     if (active)
-        run_private_lane<ENV, AGENT, RL_POLICY_NEURAL, SEL, ALGO, NetBin<(uint32_t)A>>(p, tabs, lane, L, C, nullptr);
+        run_private_lane<ENV, AGENT, RL_POLICY_NEURAL, SEL, ALGO, NetBin<(uint32_t)A>, false>(p, tabs, lane, L, C,
+                                                                                             nullptr);
     flush_stats(p, L, C, active, ACC);
 }
 // the register-resident network kernel exists for these instantiations; the host
@@ -2297,7 +2298,9 @@ __global__ void __launch_bounds__(256) k_train_private_lds(KParams p) {
 // over the lane's f64 Q / UCB counters / trace set / network in HBM.  Used by the
 // private training kernel (K steps per launch) and by the per-call Agent surface
 // (k_agent_call: rl_agent_get_action / rl_agent_update).
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane>
+// PLAN: the Dyna model code compiled in (k_train_private_net, whose registers hold
+// the network, runs only agents without planning: launch_train)
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET = NetLane, bool PLAN = true>
 struct PrivAgent {
     using E = EnvDev<ENV>;
     static constexpr int A = E::A;
@@ -2324,13 +2327,13 @@ struct PrivAgent {
         : p(p_), lane(lane_), Ls(p_.L), SA(p_.S * (uint32_t)A), L(L_), C(C_),
           t(UCB ? p_.t_priv[lane_] : 0), tcnt(AGENT == RL_AGENT_TRACES ? p_.tcnt[lane_] : 0u),
           net(NET::template make<A>(p_, lane_)), qb(qb_) {
-        if (p.plan_steps) mc = p.mcnt[lane];
+        if (PLAN && p.plan_steps) mc = p.mcnt[lane];
     }
     __device__ __forceinline__ void store() {
         if (UCB) p.t_priv[lane] = t;
         if (AGENT == RL_AGENT_TRACES) p.tcnt[lane] = tcnt;
         if constexpr (NEURAL) net.store(p, lane);
-        if (p.plan_steps) p.mcnt[lane] = mc;
+        if (PLAN && p.plan_steps) p.mcnt[lane] = mc;
     }
     // the model slot of (s, a), read at the start of a training step so its HBM
     // round trip overlaps the env step, the selection and the update
@@ -2474,7 +2477,7 @@ struct PrivAgent {
     __device__ __forceinline__ double train_update(uint32_t s, uint32_t a, double r, bool term, uint32_t s2,
                                                    uint32_t a2) {
         const double td = update(s, a, r, term, s2, a2);
-        if (p.plan_steps) {
+        if (PLAN && p.plan_steps) {
             const uint32_t key = s * A + a;
             uint4 *const mrec = p.mrec + lane * (uint64_t)SA;     // the lane's model, lane-major
             uint32_t *const mslot = p.mslot + lane * (uint64_t)SA;
@@ -2546,11 +2549,11 @@ struct PrivAgent {
 };
 
 // one private lane (a whole reference agent) for K synchronous steps, its Q at qb
-template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET>
+template <int ENV, int AGENT, int POLICY, int SEL, int ALGO, class NET, bool PLAN>
 __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTables &tabs, uint64_t lane,
                                                  LaneRegs &L, Counters &C, double *qb) {
     using E = EnvDev<ENV>;
-    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO, NET> ag(p, lane, L, C, qb);
+    PrivAgent<ENV, AGENT, POLICY, SEL, ALGO, NET, PLAN> ag(p, lane, L, C, qb);
     for (uint32_t k = 0; k < p.K; ++k) {
         if (L.mode == RL_MODE_DONE) {
             if (p.rec) write_record(p, k, lane, 0u, 0u, 0u, 0u, 0u, 0.0, false, 0.0, RL_MODE_DONE);
@@ -2567,7 +2570,7 @@ __device__ __forceinline__ void run_private_lane(const KParams &p, const EnvTabl
             continue;
         }
         const uint32_t mode_before = L.mode;      // STEP: src/agent.rs:88-101
-        if (p.plan_steps && L.mode == RL_MODE_TRAIN) ag.model_prefetch(L.s, L.a);
+        if (PLAN && p.plan_steps && L.mode == RL_MODE_TRAIN) ag.model_prefetch(L.s, L.a);
         uint32_t s2 = 0;
         double r = 0.0;
         bool term = false;
@@ -2642,7 +2645,7 @@ hipError_t launch_train(const KParams &p, dim3 grid, dim3 block, size_t smem, hi
         if constexpr (POLICY != RL_POLICY_NEURAL && ENV != RL_ENV_TAXI && ENV != RL_ENV_BLACKJACK)
             if (p.priv_lpw) k = (const void *)k_train_private_lds<ENV, AGENT, POLICY, SEL, ALGO>;
         if constexpr (use_net_regs<ENV, AGENT, POLICY>())
-            if (p.net_regs) k = (const void *)k_train_private_net<ENV, AGENT, SEL, ALGO>;
+            if (p.net_regs && p.plan_steps == 0) k = (const void *)k_train_private_net<ENV, AGENT, SEL, ALGO>;
     } else if (instr) {
         k = shared_kernel<ENV, AGENT, POLICY, SEL, ALGO, true>(p);
     } else {
