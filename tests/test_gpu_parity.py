@@ -310,8 +310,12 @@ def test_episode_log_matches_oracle(rl, oracle, case):
                                   dict(env="taxi", selector="ucb", algo="expected_sarsa"),
                                   dict(env="frozen_lake", map8x8=1, slippery=1, agent="traces",
                                        policy="double", algo="sarsa"),
-                                  dict(env="blackjack", policy="double", algo="qlearning")],
-                         ids=["cw-q", "taxi-ucb-es", "fl-traces-double", "bj-double"])
+                                  dict(env="blackjack", policy="double", algo="qlearning"),
+                                  # one-step, one table: the pipelined planning batch (reads
+                                  # ahead of the previous write, forwarded) for each TD target
+                                  dict(env="cliff_walking", algo="sarsa"),
+                                  dict(env="frozen_lake", map8x8=1, slippery=1, algo="expected_sarsa")],
+                         ids=["cw-q", "taxi-ucb-es", "fl-traces-double", "bj-double", "cw-sarsa", "fl-es"])
 def test_dyna_matches_oracle(rl, oracle, case):
     """InternalModelAgent + RandomModel, 10 planning steps (private agents):
     records, Q, ε and stats bit-exact vs the oracle (itself == the faithful loop)."""
