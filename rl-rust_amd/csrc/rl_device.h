@@ -799,6 +799,16 @@ template <> struct EnvDev<RL_ENV_TAXI> {
         term = (w & (1u << 11)) != 0;
         pos = s2;
     }
+    // step() with the transition word already read (taxi_word(pos, a) == the table's word)
+    __device__ static __forceinline__ void step_word(uint32_t &z, uint32_t w, const EnvTables &t, uint32_t &s2,
+                                                     double &rew, bool &term) {
+        if (z >= t.max_steps) { s2 = 0; rew = 0.0; term = true; return; }  // :146-149
+        z += 1;
+        s2 = w & 511u;
+        const uint32_t rc = (w >> 9) & 3u;
+        rew = rc == 0 ? -1.0 : (rc == 1 ? -10.0 : 20.0);
+        term = (w & (1u << 11)) != 0;
+    }
 };
 
 // BlackJackEnv (src/env/blackjack.rs): infinite deck, cards 1..=10 uniform.

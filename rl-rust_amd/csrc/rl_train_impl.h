@@ -87,6 +87,9 @@ __host__ __device__ constexpr bool pair_pool_env(int env) {
 #ifndef RLAMD_LATE_B3
 #define RLAMD_LATE_B3 1   // the step-separating barrier after the next step's env step
 #endif
+#ifndef RLAMD_TAXI_PF
+#define RLAMD_TAXI_PF 1   // Taxi: the next step's transition word read from the HBM table after the selection
+#endif
 #ifndef RLAMD_TRPF
 #define RLAMD_TRPF 0   // 1: FrozenLake reads the next step's transition word after the selection
                        // (cfg 2: 0.2122-0.2139 ms against 0.2116-0.2125 without, A/B on one box)
@@ -1200,6 +1203,13 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
                           (ENV == RL_ENV_FROZEN_LAKE || ENV == RL_ENV_FROZEN_LAKE_EDITED);
     uint32_t wpf = 0;
     if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, L.s, L.a)];
+    // Taxi: the transition word of the lane's (s, a) from the host's table (HBM, 12 KB:
+    // L2-resident), read one step ahead — after the selection that fixes the next
+    // step's action — instead of decoding / encoding the state (rl_taxi.h taxi_word,
+    // which the host checked equal to the table); not with the reset-and-step schedule
+    constexpr bool TXPF = RLAMD_TAXI_PF && ENV == RL_ENV_TAXI && (UCB || RS == 0);
+    uint32_t wtx = 0;
+    if constexpr (TXPF) wtx = p.trans[(L.s < S ? L.s : 0u) * (uint32_t)A + (L.a < (uint32_t)A ? L.a : 0u)];
     // reset-and-step in effect (uniform over the block)
     const bool rs_on = (!UCB && RS != 0) && (RS == 1 || p.reset_step);
     for (uint32_t k = 0; k < p.K; ++k) {
@@ -1277,7 +1287,8 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
             L.ready = true;
         } else if (doS) {
             uint32_t pos = L.s;
-            E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
+            if constexpr (TXPF) E::step_word(L.z, wtx, tabs, s2, r, term);
+            else E::template step<SLIP, LDS_AM>(pos, L.z, L.a, L.rng, tabs, s2, r, term);
             if (term) L.ready = false;
         }
         // the previous step's settle (Q, flags, counters) before this step's reads:
@@ -1367,6 +1378,7 @@ __device__ __forceinline__ void train_shared_body(const KParams &p) {
         // the next step's table word (s2, a2) read now: the table is constant, and
         // the read's latency then overlaps the update and its barriers
         if constexpr (TRPF) wpf = tabs.trans[tidx<LDS_AM, 4>(tabs, s2, a2)];
+        if constexpr (TXPF) wtx = p.trans[s2 * (uint32_t)A + a2];
         uint32_t d_own = 0xffffffffu;   // SPEC: the step-count entry this lane folds at step end
         if constexpr (SPEC) {
             // the step's increments go to the step counts / T[1], apart from what this
