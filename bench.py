@@ -13,7 +13,10 @@ cliffwalking_model's Dyna-Q (InternalModelAgent, 10 planning steps); 8 is cfg 3'
 Taxi + UCB with Q-learning, where Q stays finite (UCB's ln / sqrt / divide timed).
 
   python bench.py [--gpus N --steps K --warmup W]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N>1: bench.py --gpus N starts its N ranks itself, or runs as one of them under
+       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  At N>1 the default is the metric's fixed global lane set (strong scaling,
+  GLOBAL_LANES: 2^20 for cfg 2); --lanes L gives weak scaling at L lanes per GPU.
 
 No PyTorch: the stream, the kernel timing (HIP events, rl_agent_get_timing) and,
 for N>1, the communicator all come from librlamd.
@@ -48,7 +51,11 @@ HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks, one process per GPU). Under a launcher (WORLD_SIZE set) it must equal "
+                         "WORLD_SIZE; without one, N > 1 starts the N ranks itself (self_launch)")
+    ap.add_argument("--child-timeout", type=float, default=1500.0,
+                    help="self-launch: seconds before every rank is killed and the run fails")
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7, 8],
@@ -79,6 +86,7 @@ def parse():
     ap.add_argument("--counters-file", default=os.path.join(ROOT, "profiles", "counters.json"),
                     help="PMC summaries per workload (scripts/collect_counters.py)")
     a = ap.parse_args()
+    a.user_lanes = a.lanes is not None
     for k, v in PRESETS[a.config].items():
         if k not in ("reset_step", "extra") and getattr(a, k) is None:
             setattr(a, k, v)
@@ -121,6 +129,76 @@ PRESETS = {
     8: dict(env="taxi", agent="one_step", policy="tabular", selector="ucb", algo="qlearning",
             lanes=1 << 20, group=512),
 }
+
+
+# BASELINE.json's global lane count per workload ("2^20 envs, 1/2/4/8 GPUs"; cfg 4 "2^19 envs,
+# 4xMI355X"; cfg 5 "2^22 envs across 8xMI355X"): at N > 1 ranks the default is strong scaling over
+# this fixed set (each rank 1/N of it); --lanes L makes it weak scaling at L lanes per GPU
+GLOBAL_LANES = {2: 1 << 20, 3: 1 << 20, 4: 1 << 19, 5: 1 << 22, 6: 1 << 20, 7: 1 << 20, 8: 1 << 20}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n, timeout):
+    """`bench.py --gpus N` with no launcher: start N ranks of this same command (one
+    process per GPU: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run
+    sets them), relay rank 0's JSON line, and fail (non-zero) when any rank fails or
+    the run outlives `timeout`.  This process never touches the GPU (it imports
+    neither rlamd nor torch): the ranks are fresh children, not an exec."""
+    import tempfile
+    port = _free_port()
+    procs, outs = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = tempfile.TemporaryFile(mode="w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out, cwd=ROOT))
+    t0, rc = time.time(), 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            print(f"bench.py: a rank exited with {rc}; stopping the others", file=sys.stderr)
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() - t0 > timeout:
+            rc = 124
+            print(f"bench.py: ranks still running after {timeout:.0f} s; stopping them", file=sys.stderr)
+            break
+        time.sleep(0.05)
+    for p in procs:                       # the exact children started above, nothing else
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    texts = []
+    for out in outs:
+        out.seek(0)
+        texts.append(out.read())
+    for r, text in enumerate(texts[1:], 1):
+        if text:
+            sys.stderr.write(f"[rank {r} stdout]\n{text}")
+    if rc == 0 and not any(l.startswith("{") for l in texts[0].splitlines()):
+        print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
+        rc = 1
+    (sys.stdout if rc == 0 else sys.stderr).write(texts[0])
+    sys.stdout.flush()
+    return 0 if rc == 0 else (rc if rc > 0 else 1)
 
 
 def workload_key(args):
@@ -391,7 +469,14 @@ def rccl_bootstrap(rank, world, dev):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(self_launch(args.gpus, args.child_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    if world > 1 and args.lanes_total is None and not args.user_lanes:
+        # the metric's fixed global lane set (BASELINE.json: "2^20 envs, 1/2/4/8 GPUs")
+        args.lanes_total = GLOBAL_LANES[args.config]
     # RLAMD_FORCE_COMM=1 (tests): take the multi-GPU code path (librlamd's RCCL
     # communicator attached) even with one rank
     dist_on = world > 1 or os.environ.get("RLAMD_FORCE_COMM") == "1"

@@ -96,18 +96,39 @@ def test_bench_rccl_path_one_rank():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra,fixture,scaling", [([], "cfg2_L2M_25", "weak"),
-                                                    (["--lanes-total", str(1 << 20)], "cfg2_L1M_25", "strong")],
-                         ids=["weak-2x2^20", "strong-2^20"])
+@pytest.mark.parametrize("extra,fixture,scaling", [(["--lanes", str(1 << 20)], "cfg2_L2M_25", "weak"),
+                                                    ([], "cfg2_L1M_25", "strong")],
+                         ids=["weak-2x2^20", "strong-2^20-default"])
 def test_bench_two_ranks_q_check_matches_one_process(extra, fixture, scaling):
     """a 2-rank bench run in the driver's shape (--steps 20
     --warmup 5) ends with the merged Q of ONE process over its global lane set:
     every rank holds the same digest and it equals the oracle's for that set
-    (tests/golden/global_q.json) — weak (2 x 2^20 lanes) and the north star's
-    strong split of 2^20 lanes"""
+    (tests/golden/global_q.json) — weak (--lanes: 2 x 2^20 lanes) and the
+    default at N > 1, the metric's fixed 2^20 lanes split over the ranks (strong)"""
     r = _torchrun(["bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu-baseline"] + extra)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
     qc = d["q_check"]
     assert d["scaling"] == scaling and qc["global_lanes"] == (2 << 20 if scaling == "weak" else 1 << 20)
     assert qc["ranks_agree"] is True and qc["fixture"] == fixture and qc["match"] is True, json.dumps(qc)
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_self_launch_strong_default():
+    """`bench.py --gpus 2` with NO launcher starts its two ranks
+    itself and, by default, splits BASELINE's fixed 2^20 lanes over them (strong
+    scaling): one JSON line, n_gpus 2, the merged Q equal to the oracle's one-process
+    answer for 2^20 lanes over the driver's 25 launches (cfg2_L1M_25)"""
+    env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", RLAMD_COLLECTIVE="torch")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5",
+                        "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    qc = d["q_check"]
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["lanes_total"] == 1 << 20, d["config"]
+    assert d["config"]["lanes_per_gpu"] == 1 << 19 and d["config"]["parallelism"] == "dp2"
+    assert qc["ranks_agree"] is True and qc["fixture"] == "cfg2_L1M_25" and qc["match"] is True, json.dumps(qc)
