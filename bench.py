@@ -442,6 +442,15 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     return out
 
 
+def collective_name(collective, merge_path):
+    if collective == "torch":
+        return "torch all_reduce (rehearsal)"
+    how = {"peer": "one-shot peer-read reduce of the merge buffer over IPC-mapped exchange regions (librlamd)",
+           "rccl": "rccl int64 all-reduces of the merge buffer (librlamd)",
+           "local": "none (one rank)"}[merge_path]
+    return how + ("; rccl control plane" if collective == "rccl" else "; gloo control plane")
+
+
 def rccl_bootstrap(rank, world, dev):
     """RCCL communicator without a torch control plane: rank 0's unique id is handed
     to the other ranks through a file (one node: every rank shares /tmp), keyed by
@@ -489,10 +498,11 @@ def main():
                              f"learner groups of {args.group}")
         args.lanes = args.lanes_total // world
         scaling = "strong"
-    # collective "rccl" (default): librlamd's own RCCL all-reduce in every merge,
-    # and its communicator also runs the barriers and the max-over-ranks time —
-    # no PyTorch anywhere.  "torch": a torch.distributed all_reduce of the merge
-    # buffer, a rehearsal for ranks sharing one GPU, where RCCL cannot run.
+    # collective "rccl" (default): librlamd's own communicator — the merges by the
+    # peer-read reduce (or RCCL all-reduces), the barriers and the max-over-ranks
+    # time by RCCL — no PyTorch anywhere.  "peer": the peer-read merge with a gloo
+    # control plane, for ranks sharing one GPU (RCCL refuses them).  "torch": a
+    # torch.distributed all_reduce of the merge buffer, the same rehearsal.
     collective = os.environ.get("RLAMD_COLLECTIVE", "rccl")
     torch = dist = None
     if dist_on and collective != "rccl":
@@ -522,7 +532,17 @@ def main():
     delta, comm = None, None
     if dist_on and collective == "rccl":
         comm = rccl_bootstrap(rank, world, dev)
-        agent.set_comm(comm)                # every merge: RCCL all-reduces over xGMI, then apply
+        # every merge: the one-shot peer-read reduce over xGMI (rl.h ABI 7, set up by
+        # set_comm at world > 1 after a self-test agreed by every rank), or RCCL
+        # all-reduces (RLAMD_MERGE=rccl, or when the self-test fails); then apply
+        agent.set_comm(comm)
+    elif dist_on and collective == "peer":
+        # ranks sharing one GPU (RCCL refuses them): the peer-read merge with the
+        # exchange regions' handles all-gathered over gloo, the control plane gloo
+        hs = [None] * world
+        dist.all_gather_object(hs, agent.peer_handle())
+        agent.peer_attach(rank, world, hs)
+        agent.set_merge_groups(world * ((args.lanes + args.group - 1) // args.group))
     elif dist_on:
         # rehearsal: torch's HIP runtime (its wheel's own) and librlamd's are not one
         # runtime, so their streams do not order each other: every hand-over below is
@@ -532,6 +552,7 @@ def main():
         agent.set_delta_buffer(delta.data_ptr(), delta.numel())
         agent.set_merge_groups(world * ((args.lanes + args.group - 1) // args.group))
     mw = agent.delta_max_words()
+    merge_path = agent.merge_path() if delta is None else "torch"
 
     def step():
         if delta is None:                   # launch + merge (librlamd: RCCL all-reduces when world > 1)
@@ -637,8 +658,8 @@ def main():
                    "group_size": args.group, "sync_every": args.sync,
                    "env_steps_per_launch": steps_done / args.steps,
                    "sync_steps_per_launch": args.sync, "parallelism": f"dp{world}",
-                   "collective": ("rccl int64 all-reduces of the merge buffer (librlamd)" if collective == "rccl"
-                                  else "torch all_reduce (rehearsal)") if dist_on else "none",
+                   "collective": collective_name(collective, merge_path) if dist_on else "none",
+                   "merge_path": merge_path,
                    "groups_per_cu": occ["groups_per_cu"], "lds_bytes_per_group": occ["lds_bytes"],
                    "q_repr": q_repr, "q_mode": args.q_mode},
         "q_check": q_check,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 6
+#define RL_ABI_VERSION 7
 
 enum rl_status {
     RL_OK = 0,
@@ -395,6 +395,28 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c);
 /* the merge of one rl_agent_launch_train: all-reduce the delta over the attached
  * communicator (none: this rank alone) on the agent's stream, then Q_base += Δ */
 int rl_agent_sync(rl_agent *a);
+
+/* -------- ABI 7: the one-shot peer-read merge
+ * The merge buffers are small (cfg 2: 6 KB), so a ring all-reduce's 2(N-1) hop
+ * latencies dominate it.  Instead every rank exports an exchange region by IPC;
+ * a merge copies the rank's words into it, raises the rank's epoch flag
+ * (system-scope release) and one kernel per rank reads all N ranks' words in rank
+ * order over xGMI (int64 sums / maxima: exact, order-free) into the merge buffer.
+ * rl_agent_set_comm sets this up by itself at world > 1 (the handles travel over
+ * RCCL; a self-test merge agreed by every rank decides, RCCL stays on failure or
+ * with RLAMD_MERGE=rccl).  Without a communicator (ranks sharing one GPU, where
+ * RCCL refuses two ranks) the caller exchanges the handles:
+ *   rl_agent_peer_handle on every rank -> all-gather them (rank order) ->
+ *   rl_agent_peer_attach on every rank; then rl_agent_run / train / evaluate /
+ *   rl_agent_sync merge over the peers.  Every rank must make the same merges. */
+#define RL_PEER_HANDLE_BYTES 64
+int rl_agent_peer_handle(rl_agent *a, void *handle_out /* RL_PEER_HANDLE_BYTES */);
+int rl_agent_peer_attach(rl_agent *a, int32_t rank, int32_t world,
+                         const void *handles /* world x RL_PEER_HANDLE_BYTES, rank order */);
+/* how this agent's merges are reduced: 0 this rank alone, 1 RCCL all-reduce,
+ * 2 peer-read (above) */
+enum rl_merge_path { RL_MERGE_LOCAL = 0, RL_MERGE_RCCL = 1, RL_MERGE_PEER = 2 };
+int rl_agent_merge_path(rl_agent *a, int32_t *path);
 
 /* -------- multi-GPU: the merge as an external collective (shared mode) */
 /* int64 words of the merge buffer the current Q representation uses (all of it)

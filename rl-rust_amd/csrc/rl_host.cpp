@@ -393,6 +393,9 @@ struct rl_env {
     double *rew_d = nullptr;
     uint8_t *term_d = nullptr;
     std::vector<uint8_t> ready;
+    // a view's lanes moved under it (a train launch of its agent): ready is re-read
+    // from the lane records (LF_READY) before the next call uses it
+    bool ready_stale = false;
     KParams kp{};
 };
 
@@ -471,13 +474,35 @@ struct rl_agent {
     // whose register-limited residencies differ; the launch takes its own
     size_t smem_v[2] = {0, 0};
     uint32_t trc_kb_v[2] = {0, 0};
+    // pair-trace LDS slots per lane of the last launch (PairCache::cap; UINT32_MAX
+    // before the first): a launch with another cap re-indexes the HBM slots first
+    uint32_t pair_cap_last = UINT32_MAX;
     rl_comm *comm = nullptr;   // multi-GPU: the merge delta is all-reduced over it
+    // the one-shot peer-read merge (rl.h ABI 7, rl_misc.hip k_peer_reduce): this
+    // rank's IPC-exported exchange region and every rank's mapping of it
+    struct PeerMerge {
+        int64_t *region = nullptr;           // [2 slots][cap] words, then the epoch flag
+        uint64_t cap = 0;                    // words per slot
+        int32_t rank = 0, world = 1;
+        std::vector<int64_t *> bases;        // rank order; the peers' are IPC mappings
+        int64_t **bases_d = nullptr;
+        uint32_t *err_d = nullptr;           // a wait that timed out
+        int64_t epoch = 0;                   // merges made (every rank makes the same)
+        int64_t timeout_ticks = 0;           // wall-clock ticks a rank waits for a peer
+        bool on = false;
+    } peer;
     double q_abs0 = 0.0;       // shared mode: max |Q| the table was last reset / set to (delta_bound's Q0)
 };
 
 namespace {
 
 void agent_sync_params(rl_agent *a);
+// the peer-read merge's region handling (defined with the ABI 7 calls below)
+int peer_alloc(rl_agent *a);
+void peer_detach(rl_agent *a);
+void peer_free(rl_agent *a);
+int peer_check(rl_agent *a);
+int peer_selftest(rl_agent *a, bool *ok);
 
 int agent_select_kernel(rl_agent *a) {
     a->fn = lookup_train(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector, a->cfg.algo,
@@ -890,11 +915,28 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
         a->kp.trc_kb = a->trc_kb_v[a->kp.episodic];
         a->smem = a->smem_v[a->kp.episodic];
     }
+    // the pair lists' LDS slot count follows the carve, which differs
+    // between the kernel families and changes with the selector / representation,
+    // while a lane's list survives the launch boundary (p.tcnt).  The HBM slots'
+    // index (slot_of) and visited-state bitmap (vbits) are kept only for slots >=
+    // cap, so a launch with another cap rebuilds them for its own first
+    if (!a->priv && a->vbits && a->tcnt && pair_slot_index_env(a->cfg.env.kind) &&
+        layout_sparse_traces(a->cfg.agent, a->cfg.selector, a->cfg.algo, 0)) {
+        const uint32_t cap = shared_pair_cap(a->cfg.env.kind, a->cfg.agent, a->cfg.policy, a->cfg.selector,
+                                             a->cfg.algo, a->S, a->A, (uint32_t)a->eh.cdf.size(), a->block.x,
+                                             a->kp.trc_kb, a->qrepr == RL_QREPR_F64, a->kp.ucb_pack);
+        if (a->pair_cap_last != UINT32_MAX && cap != a->pair_cap_last) {
+            launch_pair_reindex(a->kp, cap, a->stream);
+            HIPC(hipGetLastError());
+        }
+        a->pair_cap_last = cap;
+    }
     if (a->recording) a->kp.rec = a->rec_d; else a->kp.rec = nullptr;
     // the launch moves the lanes an Env view shares: a lane the view
-    // once reset may have terminated since, so the view must reset before stepping
-    // again (the reference's Err(EnvNotReady), src/env.rs:17,24)
-    if (a->env_view) a->env_view->ready.assign(a->L, 0);
+    // once reset may have terminated since (the reference's Err(EnvNotReady),
+    // src/env.rs:17,24), and one still mid-episode may keep stepping:
+    // the view re-reads each lane's LF_READY after the launch (view_ready_refresh)
+    if (a->env_view) a->env_view->ready_stale = true;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (a->timing) {
         HIPC(hipEventCreate(&e0));
@@ -916,7 +958,8 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
         if (a->qrepr == RL_QREPR_F64) {   // f64 merge, first phase (UCB: ΔN / Δt from the replicas)
             if (a->cfg.selector == RL_SEL_UCB) launch_fold_replicas(a->kp, a->stream);
             launch_fq_merge_a(a->kp, a->stream);
-        } else if (merge && a->delta_max == a->delta_own && a->cfg.selector != RL_SEL_UCB && !a->comm) {
+        } else if (merge && a->delta_max == a->delta_own && a->cfg.selector != RL_SEL_UCB && !a->comm &&
+                   !a->peer.on) {
             launch_fold_apply(a->kp, a->stream);   // fold the replicas and apply (eps-greedy: sums + counts only)
             *merge = true;
         } else {
@@ -958,19 +1001,35 @@ int launch_apply_kernel(rl_agent *a) {
 // NaN / inf counts) over every rank.  Exact int64 arithmetic, so Q is
 // bit-identical for any rank count at a fixed global lane set.
 int comm_live(rl_agent *a);
+// the peer-read all-reduce of n int64 words of buf, in place on the agent's stream
+// (rl.h ABI 7; the protocol is at k_peer_reduce): the words to this rank's slot,
+// then one kernel raises its flag, waits for every peer's and reduces in rank order
+int peer_allreduce(rl_agent *a, int64_t *buf, uint64_t n, bool op_max) {
+    auto &pm = a->peer;
+    if (n > pm.cap) return fail(RL_E_STATE, "merge buffer larger than the peer exchange slots");
+    const uint64_t slot = (uint64_t)(pm.epoch & 1) * pm.cap;
+    ++pm.epoch;
+    launch_peer_put(buf, pm.region + slot, n, a->stream);
+    launch_peer_reduce(pm.bases_d, (uint32_t)pm.world, (uint32_t)pm.rank, slot, 2 * pm.cap + 16, n, pm.epoch,
+                       op_max ? 1 : 0, buf, pm.err_d, pm.timeout_ticks, a->stream);
+    HIPC(hipGetLastError());
+    return RL_OK;
+}
 int allreduce_max(rl_agent *a) {
-    if (!a->comm || a->qrepr != RL_QREPR_F64) return RL_OK;
-    if (int rc = comm_live(a)) return rc;
+    if ((!a->comm && !a->peer.on) || a->qrepr != RL_QREPR_F64) return RL_OK;
     uint64_t mw, sw;
     merge_layout(a, &mw, &sw);
+    if (a->peer.on) return peer_allreduce(a, a->delta_max, mw, true);
+    if (int rc = comm_live(a)) return rc;
     NCCLC(ncclAllReduce(a->delta_max, a->delta_max, mw, ncclInt64, ncclMax, a->comm->comm, a->stream));
     return RL_OK;
 }
 int allreduce_delta(rl_agent *a) {
-    if (!a->comm) return RL_OK;   // no communicator: this process's delta is the total
-    if (int rc = comm_live(a)) return rc;
+    if (!a->comm && !a->peer.on) return RL_OK;   // no communicator: this process's delta is the total
     uint64_t mw, sw;
     merge_layout(a, &mw, &sw);
+    if (a->peer.on) return peer_allreduce(a, a->delta, sw, false);
+    if (int rc = comm_live(a)) return rc;
     NCCLC(ncclAllReduce(a->delta, a->delta, sw, ncclInt64, ncclSum, a->comm->comm, a->stream));
     return RL_OK;
 }
@@ -999,7 +1058,11 @@ int allreduce_u64(rl_agent *a, uint64_t v, uint64_t *sum) {
     if (int rc = comm_live(a)) return rc;
     int64_t x = (int64_t)v;
     HIPC(hipMemcpyAsync(a->comm->word, &x, 8, hipMemcpyHostToDevice, a->stream));
-    NCCLC(ncclAllReduce(a->comm->word, a->comm->word, 1, ncclInt64, ncclSum, a->comm->comm, a->stream));
+    if (a->peer.on) {
+        if (int rc = peer_allreduce(a, a->comm->word, 1, false)) return rc;
+    } else {
+        NCCLC(ncclAllReduce(a->comm->word, a->comm->word, 1, ncclInt64, ncclSum, a->comm->comm, a->stream));
+    }
     HIPC(hipMemcpyAsync(&x, a->comm->word, 8, hipMemcpyDeviceToHost, a->stream));
     HIPC(hipStreamSynchronize(a->stream));
     *sum = (uint64_t)x;
@@ -1048,7 +1111,9 @@ int run_until_done(rl_agent *a, rl_stats *out) {
         if ((rc = launch_and_merge(a))) return abort_comm(a, rc);
         launch_ctl_word(a->kp, a->ctl_d, a->L, status, a->stream);
         if (hipGetLastError() != hipSuccess) return abort_comm(a, fail(RL_E_HIP, "control word launch"));
-        if (a->comm) {
+        if (a->peer.on) {
+            if ((rc = peer_allreduce(a, a->ctl_d, 3, false))) return abort_comm(a, rc);
+        } else if (a->comm) {
             const ncclResult_t nr = ncclAllReduce(a->ctl_d, a->ctl_d, 3, ncclInt64, ncclSum, a->comm->comm, a->stream);
             if (nr != ncclSuccess) return abort_comm(a, fail(RL_E_RCCL, std::string("control all-reduce: ") +
                                                                           ncclGetErrorString(nr)));
@@ -1269,6 +1334,17 @@ int env_stream(rl_env *e, hipStream_t *st) {
     HIPC(hipSetDevice(e->device));
     return RL_OK;
 }
+// a view after its agent's launches: every lane's readiness from its record
+// (the kernels keep LF_READY: set by a reset, cleared by a terminating step)
+int view_ready_refresh(rl_env *e, hipStream_t st) {
+    if (!e->view || !e->ready_stale) return RL_OK;
+    std::vector<uint4> core(e->L);
+    HIPC(hipMemcpyAsync(core.data(), e->kp.core, (size_t)e->L * sizeof(uint4), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < e->L; ++i) e->ready[i] = (core[i].y & LF_READY) ? 1 : 0;
+    e->ready_stale = false;
+    return RL_OK;
+}
 }  // namespace
 
 int rl_env_reset(rl_env *e, uint64_t *obs) {
@@ -1281,17 +1357,19 @@ int rl_env_reset(rl_env *e, uint64_t *obs) {
     HIPC(hipStreamSynchronize(st));
     for (uint32_t i = 0; i < e->L; ++i) obs[i] = rl_obs_to_reference(e->cfg.kind, (uint32_t)obs[i]);
     std::fill(e->ready.begin(), e->ready.end(), 1);
+    e->ready_stale = false;
     return RL_OK;
 }
 
 int rl_env_step(rl_env *e, const uint32_t *act, uint64_t *obs, double *rew, uint8_t *term) {
     if (!e || !act || !obs || !rew || !term) return fail(RL_E_ARG, "null argument");
+    hipStream_t st;
+    if (int rc = env_stream(e, &st)) return rc;
+    if (int rc = view_ready_refresh(e, st)) return rc;
     for (uint32_t i = 0; i < e->L; ++i) {
         if (!e->ready[i]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(i));
         if (act[i] >= e->eh.A) return fail(RL_E_ARG, "action out of range");
     }
-    hipStream_t st;
-    if (int rc = env_stream(e, &st)) return rc;
     HIPC(hipMemcpyAsync(e->act_d, act, e->L * 4, hipMemcpyHostToDevice, st));
     launch_env_step(e->cfg.kind, e->kp, st, e->act_d, e->obs_d, e->rew_d, e->term_d, nullptr);
     HIPC(hipGetLastError());
@@ -1313,6 +1391,7 @@ int rl_env_reset_lane(rl_env *e, uint32_t lane, uint64_t *obs) {
     if (lane >= e->L) return fail(RL_E_ARG, "lane out of range");
     hipStream_t st;
     if (int rc = env_stream(e, &st)) return rc;
+    if (int rc = view_ready_refresh(e, st)) return rc;   // the other lanes' readiness
     KParams p = e->kp;
     p.L = 1; p.core += lane; p.rng += lane;
     launch_env_reset(e->cfg.kind, p, st, e->obs_d);
@@ -1327,10 +1406,11 @@ int rl_env_reset_lane(rl_env *e, uint32_t lane, uint64_t *obs) {
 int rl_env_step_lane(rl_env *e, uint32_t lane, uint32_t action, uint64_t *obs, double *rew, uint8_t *term) {
     if (!e || !obs || !rew || !term) return fail(RL_E_ARG, "null argument");
     if (lane >= e->L) return fail(RL_E_ARG, "lane out of range");
-    if (!e->ready[lane]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(lane));
-    if (action >= e->eh.A) return fail(RL_E_ARG, "action out of range");
     hipStream_t st;
     if (int rc = env_stream(e, &st)) return rc;
+    if (int rc = view_ready_refresh(e, st)) return rc;
+    if (!e->ready[lane]) return fail(RL_E_NOT_READY, "EnvNotReady: lane " + std::to_string(lane));
+    if (action >= e->eh.A) return fail(RL_E_ARG, "action out of range");
     KParams p = e->kp;
     p.L = 1; p.core += lane; p.rng += lane;
     HIPC(hipMemcpyAsync(e->act_d, &action, 4, hipMemcpyHostToDevice, st));
@@ -1486,6 +1566,7 @@ void rl_agent_destroy(rl_agent *a) {
     dfree(a->trace); dfree(a->tlist); dfree(a->slot_of); dfree(a->tcnt); dfree(a->vbits); dfree(a->trans); dfree(a->cdf);
     dfree(a->stats_d); dfree(a->rec_d); dfree(a->elog_d); dfree(a->elog_cnt_d);
     dfree(a->mcnt); dfree(a->mrec); dfree(a->mslot);
+    peer_free(a);
     dfree(a->net_w); dfree(a->feat); dfree(a->ctl_d); dfree(a->call_d);
     if (a->call_h) (void)hipHostFree(a->call_h);
     if (a->env_view) a->env_view->owner = nullptr;   // the view outlives its agent: calls fail with RL_E_STATE
@@ -1605,7 +1686,7 @@ int rl_agent_synchronize(rl_agent *a) {
     if (!a) return fail(RL_E_ARG, "null agent");
     HIPC(hipSetDevice(a->device));
     HIPC(hipStreamSynchronize(a->stream));
-    return RL_OK;
+    return a->peer.on ? peer_check(a) : RL_OK;
 }
 
 int rl_agent_stats(rl_agent *a, rl_stats *out) {
@@ -2033,7 +2114,9 @@ int rl_agent_delta_cap_words(rl_agent *a, uint64_t *n) {
     if (!a || !n) return fail(RL_E_ARG, "null argument");
     *n = 0;
     if (a->priv) return RL_OK;
-    const uint64_t SA = (uint64_t)a->S * a->A, PSA = a->P * SA, ps = lds_entries(a);
+    // E at its largest over the selectors: Blackjack eps-greedy holds
+    // 484 compact rows per table, UCB all S, and a selector switch keeps the buffer
+    const uint64_t SA = (uint64_t)a->S * a->A, PSA = a->P * SA, ps = PSA;
     *n = std::max<uint64_t>(ps + 5 * ps + SA + 1, 2 * PSA + SA + 1);
     return RL_OK;
 }
@@ -2151,11 +2234,53 @@ int rl_comm_rank(rl_comm *c, int32_t *rank, int32_t *world) {
     return RL_OK;
 }
 
+// world > 1 over RCCL: the exchange regions' handles all-gathered over the
+// communicator, every rank attached, one self-test merge; the peer path stays on
+// only when every rank succeeded (a MIN all-reduce of the verdicts), else RCCL
+namespace {
+int comm_peer_setup(rl_agent *a) {
+    rl_comm *c = a->comm;
+    const int32_t W = c->world, R = c->rank;
+    std::vector<char> hs((size_t)W * RL_PEER_HANDLE_BYTES, 0);
+    int64_t ok = rl_agent_peer_handle(a, hs.data() + (size_t)R * RL_PEER_HANDLE_BYTES) == RL_OK ? 1 : 0;
+    char *hd = nullptr;
+    HIPC(hipMalloc((void **)&hd, hs.size()));
+    HIPC(hipMemcpyAsync(hd, hs.data(), hs.size(), hipMemcpyHostToDevice, a->stream));
+    const ncclResult_t nr = ncclAllGather(hd + (size_t)R * RL_PEER_HANDLE_BYTES, hd, RL_PEER_HANDLE_BYTES,
+                                          ncclUint8, c->comm, a->stream);
+    if (nr == ncclSuccess) HIPC(hipMemcpyAsync(hs.data(), hd, hs.size(), hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    (void)hipFree(hd);
+    if (nr != ncclSuccess) return fail(RL_E_RCCL, std::string("peer handles all-gather: ") + ncclGetErrorString(nr));
+    // every rank attaches (or fails) and then joins the agreement below
+    auto agree = [&](int64_t mine, int64_t *all) -> int {
+        HIPC(hipMemcpyAsync(c->word, &mine, 8, hipMemcpyHostToDevice, a->stream));
+        NCCLC(ncclAllReduce(c->word, c->word, 1, ncclInt64, ncclMin, c->comm, a->stream));
+        HIPC(hipMemcpyAsync(all, c->word, 8, hipMemcpyDeviceToHost, a->stream));
+        HIPC(hipStreamSynchronize(a->stream));
+        return RL_OK;
+    };
+    if (ok) ok = rl_agent_peer_attach(a, R, W, hs.data()) == RL_OK ? 1 : 0;
+    int64_t all = 0;
+    if (int rc = agree(ok, &all)) return rc;
+    if (!all) {   // some rank could not map the regions: RCCL for every rank
+        peer_detach(a);
+        return RL_OK;
+    }
+    bool good = false;
+    if (peer_selftest(a, &good) != RL_OK) good = false;
+    if (int rc = agree(good ? 1 : 0, &all)) return rc;
+    if (!all) peer_detach(a);   // (kept: the epoch count goes on from the self-test's two merges)
+    return RL_OK;
+}
+}  // namespace
+
 int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
     if (!a) return fail(RL_E_ARG, "null agent");
     if (c && a->priv) return fail(RL_E_STATE, "private mode (group_size 1) has no merge to reduce");
     if (c && c->device != a->device) return fail(RL_E_ARG, "communicator and agent on different devices");
     HIPC(hipSetDevice(a->device));
+    if (a->peer.on) peer_detach(a);
     a->comm = c;
     // the f64 merge grid's headroom counts the learner groups of every rank
     uint64_t total = a->n_groups;
@@ -2165,6 +2290,8 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
     }
     a->merge_groups = total;
     a->merge_groups_set = c != nullptr;
+    const char *mp = getenv("RLAMD_MERGE");
+    if (c && c->world > 1 && !(mp && !strcmp(mp, "rccl"))) return comm_peer_setup(a);
     return RL_OK;
 }
 
@@ -2173,6 +2300,144 @@ int rl_agent_sync(rl_agent *a) {
     if (a->priv) return RL_OK;
     HIPC(hipSetDevice(a->device));
     return merge_after_launch(a);
+}
+
+// ---------------------------------------------------------------- peer-read merge (ABI 7)
+namespace {
+// this rank's exchange region: uncached device memory (stores reach HBM, where a
+// peer's reads over xGMI see them), two slots of the largest merge buffer either
+// representation can need, and the epoch flag 128 B past them
+int peer_alloc(rl_agent *a) {
+    auto &pm = a->peer;
+    if (pm.region) return RL_OK;
+    uint64_t cap = 0;
+    if (int rc = rl_agent_delta_cap_words(a, &cap)) return rc;
+    pm.cap = std::max<uint64_t>(cap, 16);
+    const size_t bytes = (2 * pm.cap + 32) * 8;
+    if (hipExtMallocWithFlags((void **)&pm.region, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        pm.region = nullptr;
+        return fail(RL_E_OOM, "peer exchange region (uncached)");
+    }
+    HIPC(hipMemset(pm.region, 0, bytes));
+    if (hipMalloc((void **)&pm.err_d, 4) != hipSuccess) return fail(RL_E_OOM, "peer error word");
+    HIPC(hipMemset(pm.err_d, 0, 4));
+    int khz = 100000;   // the wall clock (s_memrealtime) rate
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, a->device);
+    const char *e = getenv("RLAMD_PEER_TIMEOUT_S");
+    pm.timeout_ticks = (int64_t)((e ? atof(e) : 120.0) * 1e3 * (khz > 0 ? khz : 100000));
+    return RL_OK;
+}
+void peer_detach(rl_agent *a) {
+    auto &pm = a->peer;
+    if (a->stream) (void)hipStreamSynchronize(a->stream);
+    for (int32_t r = 0; r < (int32_t)pm.bases.size(); ++r)
+        if (r != pm.rank && pm.bases[r]) (void)hipIpcCloseMemHandle(pm.bases[r]);
+    pm.bases.clear();
+    if (pm.bases_d) (void)hipFree(pm.bases_d);
+    pm.bases_d = nullptr;
+    pm.on = false;
+    pm.epoch = 0;
+    if (pm.region) (void)hipMemset(pm.region, 0, (2 * pm.cap + 32) * 8);   // flags back to epoch 0
+}
+void peer_free(rl_agent *a) {
+    peer_detach(a);
+    if (a->peer.region) (void)hipFree(a->peer.region);
+    if (a->peer.err_d) (void)hipFree(a->peer.err_d);
+    a->peer.region = nullptr;
+    a->peer.err_d = nullptr;
+}
+// a peer wait that timed out (a rank that never reached the merge)
+int peer_check(rl_agent *a) {
+    if (!a->peer.err_d) return RL_OK;
+    uint32_t err = 0;
+    HIPC(hipMemcpy(&err, a->peer.err_d, 4, hipMemcpyDeviceToHost));
+    if (err) return fail(RL_E_STATE, "peer-read merge: a rank did not arrive within RLAMD_PEER_TIMEOUT_S");
+    return RL_OK;
+}
+// a merge of known words over the peers (every rank: word i = (rank + 1)(i + 1)):
+// the sums and the maxima must come back exact, else the peers cannot see each
+// other's regions and the caller keeps RCCL
+int peer_selftest(rl_agent *a, bool *ok) {
+    auto &pm = a->peer;
+    const int n = 16;
+    std::vector<int64_t> v(2 * n), got(2 * n);
+    for (int i = 0; i < n; ++i) v[i] = v[n + i] = (int64_t)(pm.rank + 1) * (i + 1);
+    int64_t *d = nullptr;
+    HIPC(hipMalloc((void **)&d, 2 * n * 8));
+    int rc = RL_OK;
+    if (hipMemcpyAsync(d, v.data(), 2 * n * 8, hipMemcpyHostToDevice, a->stream) != hipSuccess)
+        rc = fail(RL_E_HIP, "peer self-test upload");
+    const int64_t saved = pm.timeout_ticks;
+    pm.timeout_ticks = std::min<int64_t>(saved, saved / 12 + 1);   // 10 s of the default 120
+    if (!rc) rc = peer_allreduce(a, d, n, false);
+    if (!rc) rc = peer_allreduce(a, d + n, n, true);
+    pm.timeout_ticks = saved;
+    if (!rc && hipMemcpyAsync(got.data(), d, 2 * n * 8, hipMemcpyDeviceToHost, a->stream) != hipSuccess)
+        rc = fail(RL_E_HIP, "peer self-test read");
+    if (!rc && hipStreamSynchronize(a->stream) != hipSuccess) rc = fail(RL_E_HIP, "peer self-test");
+    (void)hipFree(d);
+    if (rc) return rc;
+    uint32_t err = 0;
+    HIPC(hipMemcpy(&err, pm.err_d, 4, hipMemcpyDeviceToHost));
+    const int64_t W = pm.world;
+    *ok = err == 0;
+    for (int i = 0; i < n && *ok; ++i)
+        *ok = got[i] == (W * (W + 1) / 2) * (i + 1) && got[n + i] == W * (i + 1);
+    return RL_OK;
+}
+}  // namespace
+
+int rl_agent_peer_handle(rl_agent *a, void *handle_out) {
+    if (!a || !handle_out) return fail(RL_E_ARG, "null argument");
+    if (a->priv) return fail(RL_E_STATE, "private mode (group_size 1) has no merge to reduce");
+    HIPC(hipSetDevice(a->device));
+    if (int rc = peer_alloc(a)) return rc;
+    static_assert(sizeof(hipIpcMemHandle_t) == RL_PEER_HANDLE_BYTES, "IPC handle size");
+    hipIpcMemHandle_t h;
+    HIPC(hipIpcGetMemHandle(&h, a->peer.region));
+    memcpy(handle_out, &h, sizeof h);
+    return RL_OK;
+}
+
+int rl_agent_peer_attach(rl_agent *a, int32_t rank, int32_t world, const void *handles) {
+    if (!a || !handles || world < 1 || rank < 0 || rank >= world) return fail(RL_E_ARG, "bad rank / world / handles");
+    if (a->priv) return fail(RL_E_STATE, "private mode (group_size 1) has no merge to reduce");
+    HIPC(hipSetDevice(a->device));
+    if (int rc = peer_alloc(a)) return rc;
+    peer_detach(a);
+    auto &pm = a->peer;
+    pm.rank = rank;
+    pm.world = world;
+    pm.bases.assign(world, nullptr);
+    const char *hb = (const char *)handles;
+    for (int32_t r = 0; r < world; ++r) {
+        if (r == rank) { pm.bases[r] = pm.region; continue; }
+        hipIpcMemHandle_t h;
+        memcpy(&h, hb + (size_t)r * RL_PEER_HANDLE_BYTES, sizeof h);
+        void *p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            peer_detach(a);
+            return fail(RL_E_HIP, std::string("hipIpcOpenMemHandle (rank ") + std::to_string(r) + "): " +
+                                      hipGetErrorString(e));
+        }
+        pm.bases[r] = (int64_t *)p;
+    }
+    if (hipMalloc((void **)&pm.bases_d, world * sizeof(int64_t *)) != hipSuccess ||
+        hipMemcpy(pm.bases_d, pm.bases.data(), world * sizeof(int64_t *), hipMemcpyHostToDevice) != hipSuccess) {
+        peer_detach(a);
+        return fail(RL_E_HIP, "peer table");
+    }
+    HIPC(hipMemset(pm.err_d, 0, 4));
+    pm.epoch = 0;
+    pm.on = world > 1;
+    return RL_OK;
+}
+
+int rl_agent_merge_path(rl_agent *a, int32_t *path) {
+    if (!a || !path) return fail(RL_E_ARG, "null argument");
+    *path = a->peer.on ? RL_MERGE_PEER : (a->comm ? RL_MERGE_RCCL : RL_MERGE_LOCAL);
+    return RL_OK;
 }
 
 int rl_agent_set_stream(rl_agent *a, void *stream) {

@@ -181,6 +181,17 @@ train_launch_fn lookup_train(int env, int agent, int policy, int sel, int algo, 
 size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
                          uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack);
 size_t private_smem_bytes(int env, int agent, int policy, int sel, uint32_t S, uint32_t A, uint32_t n_start);
+// shared pair traces: LDS slots per lane for a carve, whether the env's lists use
+// the HBM slot index, and its rebuild for a new slot count (rl_misc.hip)
+uint32_t shared_pair_cap(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
+                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack);
+bool pair_slot_index_env(int env);
+void launch_pair_reindex(const KParams &p, uint32_t cap, hipStream_t s);
+// the one-shot peer-read merge (rl_misc.hip k_peer_put / k_peer_reduce)
+void launch_peer_put(const int64_t *src, int64_t *slot, uint64_t n, hipStream_t s);
+void launch_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank, uint64_t slot_off, uint64_t flag_off,
+                        uint64_t n, int64_t epoch, int op_max, int64_t *dst, uint32_t *err, int64_t timeout_ticks,
+                        hipStream_t s);
 
 // env-only kernels (batched Env trait) and KAT probes
 void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs);

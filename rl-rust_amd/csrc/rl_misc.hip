@@ -33,6 +33,46 @@ size_t shared_smem_bytes(int env, int agent, int policy, int sel, int algo, uint
     return smem_layout(env, P, ucb, traces, S, A, n_start, nthr, trc_kb, fq, ucb_pack,
                        qsh_layout(fq, ucb, P, algo) ? 1 : 0).total;
 }
+uint32_t shared_pair_cap(int env, int agent, int policy, int sel, int algo, uint32_t S, uint32_t A,
+                         uint32_t n_start, uint32_t nthr, uint32_t trc_kb, int fq, int ucb_pack) {
+    const int traces = agent != RL_AGENT_TRACES ? 0 : layout_sparse_traces(agent, sel, algo, 0) ? 2 : 1;
+    const int ucb = sel != RL_SEL_UCB ? 0 : algo == RL_ALGO_EXPECTED_SARSA ? 2 : 1;
+    const int P = policy == RL_POLICY_DOUBLE ? 2 : 1;
+    return smem_layout(env, P, ucb, traces, S, A, n_start, nthr, trc_kb, fq, ucb_pack,
+                       qsh_layout(fq, ucb, P, algo) ? 1 : 0).trc_cap;
+}
+// the envs whose shared pair lists append through pair_visit (slot_of + vbits for
+// the HBM slots); the small tables keep their pair bits in registers (PBITS in
+// train_shared_body) and never read either
+bool pair_slot_index_env(int env) {
+    return !(RLAMD_COOP_SWEEP && RLAMD_PAIR_BITS &&
+             (env == RL_ENV_CLIFF_WALKING || env == RL_ENV_FROZEN_LAKE || env == RL_ENV_FROZEN_LAKE_EDITED));
+}
+
+// ---------------------------------------------------------------- pair-trace re-index
+// A lane's pair list keeps slots [0, cap) in LDS during a launch and [cap, np) in
+// HBM with slot_of[id] and the visited-state bitmap vbits covering the HBM part
+// only (pair_visit).  Positions and first-of-state flags do not depend on cap, so
+// when a launch runs with another cap than the last (the carve of the
+// other kernel family, or a selector switch) the index of its HBM part is rebuilt
+// here: vbits cleared (a grown cap leaves bits of slots now in LDS, which the
+// episode end would no longer clear), then slot_of / vbits for [cap, np).
+__global__ void k_pair_reindex(KParams p, uint32_t cap) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= p.L) return;
+    const uint64_t Ls = p.L;
+    const uint32_t np = p.tcnt[lane], nw = (p.S + 31u) >> 5;
+    for (uint32_t w = 0; w < nw; ++w) p.vbits[(uint64_t)w * Ls + lane] = 0u;
+    for (uint32_t j = cap; j < np; ++j) {
+        const uint32_t id = p.tlist[pslot(p, j, lane)] & 0x7fffu, s = id / p.A;
+        p.slot_of[(uint64_t)id * Ls + lane] = (uint16_t)j;
+        uint32_t *vw = &p.vbits[(uint64_t)(s >> 5) * Ls + lane];
+        *vw = *vw | (1u << (s & 31u));
+    }
+}
+void launch_pair_reindex(const KParams &p, uint32_t cap, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_reindex, dim3((unsigned)((p.L + 255) / 256)), dim3(256), 0, s, p, cap);
+}
 
 // ---------------------------------------------------------------- lane init
 // Fresh lanes: RNG keyed (seed, global lane), need_reset, DoubleTabularPolicy
@@ -108,6 +148,70 @@ __global__ void __launch_bounds__(64) k_ctl_word(const unsigned long long *stats
 }
 void launch_ctl_word(const KParams &p, int64_t *ctl, uint64_t lanes, int64_t status, hipStream_t s) {
     hipLaunchKernelGGL(k_ctl_word, dim3(1), dim3(64), 0, s, p.stats, ctl, lanes, status);
+}
+
+// ---------------------------------------------------------------- peer-read merge
+// the all-reduce of a small merge buffer as one read of every rank's
+// words over xGMI.  Each rank's exchange region (uncached device memory, exported
+// by IPC; rl_host.cpp PeerMerge) holds two slots of `cap` words and, 128 B past
+// them, the rank's epoch flag.  Merge e (1, 2, ...) uses slot e & 1:
+//   k_peer_put     the rank's words -> its own slot (system-scope stores: they
+//                  reach memory, not a cache another GPU cannot see);
+//   k_peer_reduce  block 0 raises the rank's flag to e (system-scope release),
+//                  every block waits until each peer's flag is >= e (system-scope
+//                  acquire, bounded), then sums (or takes the max of) the N
+//                  ranks' words in rank order into the merge buffer — int64, so
+//                  exact and order-free.
+// Slot reuse is safe with two slots: a rank rewrites slot e & 1 at merge e + 2
+// only after its merge e + 1 saw every peer's flag at e + 1, which a peer raises
+// only after its own reads of merge e are done (same stream, in order).
+// A peer that never arrives (a crashed rank) ends the wait after timeout_ticks of
+// the wall clock with *err set, so no kernel spins forever.
+__global__ void k_peer_put(const int64_t *src, int64_t *slot, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) __hip_atomic_store(&slot[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void __launch_bounds__(256) k_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank,
+                                                     uint64_t slot_off, uint64_t flag_off, uint64_t n,
+                                                     int64_t epoch, int32_t op_max, int64_t *dst, uint32_t *err,
+                                                     int64_t timeout_ticks) {
+    __shared__ uint32_t timed_out;
+    if (threadIdx.x == 0) {
+        timed_out = 0u;
+        if (blockIdx.x == 0)
+            __hip_atomic_store(&bases[rank][flag_off], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int64_t t0 = wall_clock64();
+        for (uint32_t r = 0; r < world && !timed_out; ++r) {
+            if (r == rank) continue;
+            while (__hip_atomic_load(&bases[r][flag_off], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+                __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > timeout_ticks) {
+                    timed_out = 1u;
+                    atomicOr(err, 1u);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (timed_out || i >= n) return;
+    int64_t acc = op_max ? INT64_MIN : 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        const int64_t v = __hip_atomic_load(&bases[r][slot_off + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        acc = op_max ? (v > acc ? v : acc) : (int64_t)((uint64_t)acc + (uint64_t)v);
+    }
+    dst[i] = acc;
+}
+void launch_peer_put(const int64_t *src, int64_t *slot, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_peer_put, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, slot, n);
+}
+void launch_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank, uint64_t slot_off, uint64_t flag_off,
+                        uint64_t n, int64_t epoch, int op_max, int64_t *dst, uint32_t *err, int64_t timeout_ticks,
+                        hipStream_t s) {
+    // at least one block: block 0 raises the flag even for n == 0
+    hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)(n ? (n + 255) / 256 : 1)), dim3(256), 0, s,
+                       bases, world, rank, slot_off, flag_off, n, epoch, op_max, dst, err, timeout_ticks);
 }
 
 // ---------------------------------------------------------------- replica fold

@@ -158,7 +158,12 @@ SIGNATURES = {
     "rl_agent_set_comm": (C.c_int, [_V, _V]),
     "rl_comm_allreduce_f64": (C.c_int, [_V, _V, C.c_uint32, C.c_int32]),
     "rl_agent_sync": (C.c_int, [_V]),
+    "rl_agent_peer_handle": (C.c_int, [_V, _V]),
+    "rl_agent_peer_attach": (C.c_int, [_V, C.c_int32, C.c_int32, _V]),
+    "rl_agent_merge_path": (C.c_int, [_V, _P(C.c_int32)]),
 }
+PEER_HANDLE_BYTES = 64
+MERGE_PATHS = {0: "local", 1: "rccl", 2: "peer"}
 COMM_ID_BYTES = 128
 
 _lib = None
@@ -574,6 +579,24 @@ class Agent:
     def sync(self):
         """the merge after launch_train(): RCCL all-reduces (MAX, fold, SUM), then apply"""
         check(lib().rl_agent_sync(self.h))
+
+    # ---- ABI 7: the one-shot peer-read merge (rl.h rl_agent_peer_handle / _attach)
+    def peer_handle(self):
+        """this rank's exchange-region IPC handle (RL_PEER_HANDLE_BYTES bytes)"""
+        buf = (C.c_uint8 * PEER_HANDLE_BYTES)()
+        check(lib().rl_agent_peer_handle(self.h, buf))
+        return bytes(buf)
+
+    def peer_attach(self, rank, world, handles):
+        """every rank's handle, in rank order: from then on every merge reads the peers"""
+        assert len(handles) == world and all(len(h) == PEER_HANDLE_BYTES for h in handles)
+        buf = (C.c_uint8 * (PEER_HANDLE_BYTES * world)).from_buffer_copy(b"".join(handles))
+        check(lib().rl_agent_peer_attach(self.h, rank, world, buf))
+
+    def merge_path(self):
+        v = C.c_int32()
+        check(lib().rl_agent_merge_path(self.h, C.byref(v)))
+        return MERGE_PATHS[v.value]
 
     def set_stream(self, stream_ptr):
         check(lib().rl_agent_set_stream(self.h, C.c_void_p(stream_ptr)))

@@ -29,27 +29,46 @@ def main():
     dist.init_process_group("gloo")
     n_launch = case.pop("n_launch")
     L = case.pop("lanes_per_rank")
+    merge = case.pop("merge", "torch")
+    train_eps = case.pop("train_episodes", 0)
     p = rlamd.default_params(n_lanes=L, lane_offset=rank * L, **case)
     a = rlamd.Agent(p)
-    delta = torch.zeros(a.delta_words(), dtype=torch.int64, device="cuda:0")
-    mw = a.delta_max_words()
-    a.set_delta_buffer(delta.data_ptr(), delta.numel())
     groups = (L + case["group_size"] - 1) // case["group_size"]
-    a.set_merge_groups(world * groups)          # the f64 merge grid counts every rank's groups
-    repr_rank = a.q_repr()
-    # torch's HIP runtime (its wheel's own) and librlamd's do not order each other's
-    # streams: each hand-over synchronizes the side that wrote the buffer
-    for _ in range(n_launch):
-        a.launch_train()
+    path = None
+    if merge == "peer":
+        # rl.h ABI 7: the exchange regions' IPC handles all-gathered (here over gloo),
+        # then every merge of run() / train() reads the peers' words in the library
+        hs = [None] * world
+        dist.all_gather_object(hs, a.peer_handle())
+        a.peer_attach(rank, world, hs)
+        a.set_merge_groups(world * groups)
+        path = a.merge_path()
+        repr_rank = a.q_repr()
+        dist.barrier()
+        for _ in range(n_launch):
+            a.run(1)
+        if train_eps:
+            a.train(train_eps, 0)       # the control word summed over the peers too
         a.synchronize()
-        dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
-        torch.cuda.synchronize()
-        a.launch_fold()
+    else:
+        delta = torch.zeros(a.delta_words(), dtype=torch.int64, device="cuda:0")
+        mw = a.delta_max_words()
+        a.set_delta_buffer(delta.data_ptr(), delta.numel())
+        a.set_merge_groups(world * groups)          # the f64 merge grid counts every rank's groups
+        repr_rank = a.q_repr()
+        # torch's HIP runtime (its wheel's own) and librlamd's do not order each other's
+        # streams: each hand-over synchronizes the side that wrote the buffer
+        for _ in range(n_launch):
+            a.launch_train()
+            a.synchronize()
+            dist.all_reduce(delta[:mw], op=dist.ReduceOp.MAX)
+            torch.cuda.synchronize()
+            a.launch_fold()
+            a.synchronize()
+            dist.all_reduce(delta[mw:])
+            torch.cuda.synchronize()
+            a.launch_apply()
         a.synchronize()
-        dist.all_reduce(delta[mw:])
-        torch.cuda.synchronize()
-        a.launch_apply()
-    a.synchronize()
     q, qf = a.q_raw(), a.q()
     st = a.stats()["train_steps"]
     ucb = a.ucb() if case.get("selector") == "ucb" else None
@@ -59,6 +78,8 @@ def main():
     if rank == 0:
         one = rlamd.Agent(rlamd.default_params(n_lanes=world * L, lane_offset=0, **case))
         one.run(n_launch)
+        if train_eps:
+            one.train(train_eps, 0)
         one.synchronize()
         qf1 = one.q()
         res = {"q_equal": bool(np.array_equal(q, one.q_raw())),
@@ -69,7 +90,8 @@ def main():
                "q_nonfinite": int(np.count_nonzero(~np.isfinite(qf))),
                "q_nonzero": int(np.count_nonzero(q)),
                "q_repr": [repr_rank, one.q_repr()],
-               "steps_ranks": int(steps.item()), "steps_one": int(one.stats()["train_steps"])}
+               "steps_ranks": int(steps.item()), "steps_one": int(one.stats()["train_steps"]),
+               "merge_path": path}
         if ucb is not None:
             u1 = one.ucb()
             res["ucb_equal"] = bool(np.array_equal(ucb[0], u1[0]) and ucb[1] == u1[1])

@@ -16,6 +16,8 @@ Cases (the driver's command shape is --steps 20 --warmup 5: 25 launches):
                         --lanes-total 1048576 at any N is cfg2_L1M_25 (strong)
   cfg2_L1M_65           the default bench run (1 + 64 launches) at 2^20 lanes in total
   cfg5_L4M_25           bench.py --config 5 --gpus 8 (2^19 per GPU = BASELINE's 2^22 in total)
+  cfg4_L512K_25         bench.py --config 4 --gpus 4 (BASELINE's 2^19 envs over 4 GPUs: 2^17 per rank,
+                        the N > 1 default) and bench.py --config 4 --lanes 524288 on one GPU
 
     python tests/golden/make_global_q.py        (the 2^23-lane case is the long one: about 15 min)
 """
@@ -35,6 +37,7 @@ M = 1 << 20
 CASES = {
     "cfg2_L1M_25": (2, M, 25), "cfg2_L2M_25": (2, 2 * M, 25), "cfg2_L4M_25": (2, 4 * M, 25),
     "cfg2_L8M_25": (2, 8 * M, 25), "cfg2_L1M_65": (2, M, 65), "cfg5_L4M_25": (5, 4 * M, 25),
+    "cfg4_L512K_25": (4, M // 2, 25),
 }
 
 

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol(rl):
     assert not missing, missing
     # and the Python binding covers the whole header
     assert set(names) <= set(rl.SIGNATURES), set(names) - set(rl.SIGNATURES)
-    assert rl.lib().rl_abi_version() == 6
+    assert rl.lib().rl_abi_version() == 7
     info = rl.lib().rl_build_info().decode()
     assert "gfx950" in info and "RLAMD_EXP=0" in info and "-ffp-contract=off" in info, info
 

@@ -63,6 +63,28 @@ def test_two_rank_device_merge_equals_one_process(tmp_path, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", list(CASES))
+def test_two_rank_peer_merge_equals_one_process(tmp_path, name):
+    """VERDICT r05 item 2 / SURVEY §8(e): the one-shot peer-read merge (rl.h ABI 7:
+    IPC-exported exchange regions, epoch flags, one kernel reading both ranks' words
+    in rank order) — two processes sharing the GPU — ends every merge of run() and
+    of train() (its control word too) with the raw Q, UCB counters and step counts of
+    ONE process holding all lanes, in both representations"""
+    case = dict(CASES[name], sync_every=32, n_launch=4, lanes_per_rank=8192, merge="peer", train_episodes=3)
+    out = tmp_path / "res.json"
+    r = _torchrun([os.path.join("tests", "dist_gpu_worker.py"), str(out), json.dumps(case)])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert res["merge_path"] == "peer", res
+    assert res["steps_ranks"] == res["steps_one"] > 0, res
+    assert res["q_nonzero"] + res["q_nonfinite"] > 0, res
+    assert res["q_equal"] and res["qf_equal"], res
+    assert res["q_repr"][0] == res["q_repr"][1] == ("fixed40" if name == "fl8x8-qlearning" else "f64"), res
+    if "ucb_equal" in res:
+        assert res["ucb_equal"], res
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_prints_one_line():
     r = _torchrun(["bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1", "--lanes", str(1 << 16),
                    "--no-cpu-baseline"])
@@ -132,3 +154,23 @@ def test_bench_gpus2_self_launch_strong_default():
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["lanes_total"] == 1 << 20, d["config"]
     assert d["config"]["lanes_per_gpu"] == 1 << 19 and d["config"]["parallelism"] == "dp2"
     assert qc["ranks_agree"] is True and qc["fixture"] == "cfg2_L1M_25" and qc["match"] is True, json.dumps(qc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,fixture", [(2, "cfg2_L1M_25"), (4, "cfg4_L512K_25")], ids=["cfg2", "cfg4"])
+def test_bench_gpus2_peer_merge_q_check(config, fixture):
+    """`bench.py --gpus 2` (self-launched ranks sharing the
+    GPU) with the one-shot peer-read merge in every launch: the default strong split
+    of BASELINE's global lane set (cfg 2: 2^20; cfg 4: 2^19, "2^19 envs, 4xMI355X")
+    ends with the oracle's one-process Q for that set over the driver's 25 launches"""
+    env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", RLAMD_COLLECTIVE="peer")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--config", str(config), "--gpus", "2", "--steps", "20",
+                        "--warmup", "5", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    qc = d["q_check"]
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["merge_path"] == "peer", d["config"]
+    assert qc["ranks_agree"] is True and qc["fixture"] == fixture and qc["match"] is True, json.dumps(qc)

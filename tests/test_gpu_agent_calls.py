@@ -265,6 +265,24 @@ def test_batched_call_lengths_and_view_readiness(rl):
     assert ex.value.code == 1               # EnvNotReady until the view resets the lane
     env.reset_lane(0)
     env.step_lane(0, 1)
+    # after run() a lane still mid-episode keeps stepping (Env::step of
+    # an env that has not terminated), one that terminated needs a reset: the view
+    # follows each lane record's LF_READY bit instead of refusing every lane
+    LF_READY = 1 << 9
+    for _ in range(6):
+        agent.run(1)
+        core, _aux = agent.lane_state()
+        ready = (core[:, 1] & LF_READY) != 0
+        for lane in range(8):
+            if ready[lane]:
+                env.step_lane(lane, 1)
+            else:
+                with pytest.raises(rl.RLError) as ex:
+                    env.step_lane(lane, 1)
+                assert ex.value.code == 1
+        if ready.any() and not ready.all():
+            break
+    assert ready.any() and not ready.all(), core[:, 1]
 
 
 def fused_train(agent, n_episodes, eval_at):

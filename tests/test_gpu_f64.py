@@ -167,34 +167,51 @@ def test_train_zero_between_runs_is_a_noop(rl, oracle, G):
     _assert_stats_equal(dev, ref)
 
 
-def test_delta_cap_survives_representation_switch(rl, oracle):
-    """a caller-owned merge buffer sized by rl_agent_delta_cap_words in
-    the fixed point still fits after the table switches to f64 (here by
-    set_q_mode), and the external-collective merge then equals rl_agent_run"""
+@pytest.mark.parametrize("case", ["q_mode", "selector"])
+def test_delta_cap_survives_representation_switch(rl, oracle, case):
+    """a caller-owned merge buffer sized by rl_agent_delta_cap_words
+    before a switch still fits after it — FrozenLake's table moving from the fixed
+    point to f64 (set_q_mode), and Blackjack's selector moving from eps-greedy
+    (484 compact LDS rows per table) to UCB (all S rows) — and the
+    external-collective merge then equals rl_agent_run"""
     import ctypes as C
     # device memory from the HIP runtime librlamd itself is linked to (a torch of
     # another ROCm in the same process would bring a second runtime)
     hip = C.CDLL("libamdhip64.so")
-    p = rl.default_params(env="frozen_lake", map8x8=1, algo="qlearning", n_lanes=2048, group_size=256,
-                          sync_every=8)
+    if case == "q_mode":
+        p = rl.default_params(env="frozen_lake", map8x8=1, algo="qlearning", n_lanes=2048, group_size=256,
+                              sync_every=8)
+    else:
+        p = rl.default_params(env="blackjack", algo="qlearning", n_lanes=2048, group_size=256, sync_every=8)
     dev, ref = rl.Agent(p), oracle.Batch(p)
-    assert dev.q_repr() == "fixed40"
     cap = dev.delta_cap_words()
     assert cap >= dev.delta_words()
     buf = C.c_void_p()
     assert hip.hipMalloc(C.byref(buf), C.c_size_t(cap * 8)) == 0
-    assert hip.hipMemset(buf, 0, C.c_size_t(cap * 8)) == 0
-    dev.set_delta_buffer(buf.value, cap)
-    dev.set_merge_groups(8)
-    dev.set_q_mode("f64")
-    ref.set_q_mode("f64")
-    assert dev.q_repr() == "f64" and cap >= dev.delta_words()
-    for _ in range(3):
-        dev.launch_train()        # one rank: the collectives are the identity
-        dev.launch_fold()
-        dev.launch_apply()
-    dev.synchronize()
-    ref.run(3)
-    assert np.array_equal(dev.q_raw(), ref.q_raw())
-    dev.close()
-    hip.hipFree(buf)
+    try:
+        assert hip.hipMemset(buf, 0, C.c_size_t(cap * 8)) == 0
+        dev.set_delta_buffer(buf.value, cap)
+        dev.set_merge_groups(8)
+        if case == "q_mode":
+            assert dev.q_repr() == "fixed40"
+            dev.set_q_mode("f64")
+            ref.set_q_mode("f64")
+            assert dev.q_repr() == "f64"
+        else:   # f64 over the compact rows, then UCB's dense ones
+            dev.set_q_mode("f64")
+            ref.set_q_mode("f64")
+            before = dev.delta_words()
+            dev.set_action_selector("ucb")
+            ref.set_selector("ucb")
+            assert dev.delta_words() > before
+        assert cap >= dev.delta_words()
+        for _ in range(3):
+            dev.launch_train()        # one rank: the collectives are the identity
+            dev.launch_fold()
+            dev.launch_apply()
+        dev.synchronize()
+        ref.run(3)
+        assert np.array_equal(dev.q_raw(), ref.q_raw())
+    finally:
+        dev.close()
+        hip.hipFree(buf)

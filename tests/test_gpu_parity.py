@@ -445,6 +445,33 @@ def test_pair_trace_lds_slots(rl, oracle, trc_kb, monkeypatch):
     _assert_stats_equal(dev, ref)
 
 
+@pytest.mark.parametrize("env", ["taxi", "blackjack"])
+def test_pair_trace_cap_change_mid_episode(rl, oracle, env, monkeypatch):
+    """a lane's pair list outlives the launch (p.tcnt) while its LDS
+    slot count follows the carve, which a reconfiguration (selector / representation
+    switch, the other kernel family) can change mid-episode.  Lists then continue
+    under a grown cap (0 -> 8 KiB: HBM-indexed pairs now in LDS, stale visited-state
+    bits) and a shrunk one (8 -> 1 KiB: pairs now in HBM without slot_of): the HBM
+    index is rebuilt (k_pair_reindex) and Q stays bit-exact.  The reconfiguration is
+    set_action_selector to the same eps-greedy selector (the reference replaces the
+    selector: epsilon restarts) with RLAMD_TRC_KB changed in between."""
+    p = _params(rl, env=env, agent="traces", algo="qlearning", n_lanes=700, group_size=64, sync_every=16,
+                n_episodes_for_decay=40)
+    monkeypatch.setenv("RLAMD_TRC_KB", "0")
+    dev = rl.Agent(p)
+    ref = oracle.Batch(p)
+    for kb in ["8", "1"]:
+        dev.run(3)
+        ref.run(3)
+        monkeypatch.setenv("RLAMD_TRC_KB", kb)
+        dev.set_action_selector("eps_greedy")
+        ref.set_selector("eps_greedy")
+    dev.run(3)
+    ref.run(3)
+    assert np.array_equal(dev.q_raw(), ref.q_raw())
+    _assert_stats_equal(dev, ref)
+
+
 @pytest.mark.parametrize("terminal", ["uniform", "mixed"])
 def test_blackjack_terminal_rows_after_set_q(rl, oracle, terminal):
     """Compact Blackjack rows read terminal rows from Q_base, or from one
