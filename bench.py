@@ -229,6 +229,36 @@ def q_fixture(args, world):
     return None
 
 
+PRIVATE_Q = os.path.join(ROOT, "tests", "golden", "private_q.json")
+PRIV_WINDOW = 4096
+
+
+def private_q_check(args, agent):
+    """Private rows: the last 4096 lanes' Q (cfg 6 also their
+    network parameters), read alone (rl_agent_get_q_lanes), hashed and compared with
+    the oracle's answer for exactly those lanes (tests/golden/private_q.json,
+    tests/golden/make_private_q.py: private lanes are independent and keyed by global
+    lane id, so the oracle runs only the window)"""
+    import numpy as np
+    L = args.lanes
+    def f64_sha(x):       # NaN canonical (make_private_q.f64_sha)
+        x = np.ascontiguousarray(x, "<f8")
+        return hashlib.sha256(np.where(np.isnan(x), np.nan, x).astype("<f8").tobytes()).hexdigest()
+    qh = f64_sha(agent.q_lanes(L - PRIV_WINDOW, PRIV_WINDOW))
+    wh = f64_sha(agent.weights_lanes(L - PRIV_WINDOW, PRIV_WINDOW)) if args.policy == "neural" else None
+    fx = None
+    try:
+        tab = json.load(open(PRIVATE_Q))["cases"]
+        want = {"config": args.config, "global_lanes": L, "lane0": L - PRIV_WINDOW, "window": PRIV_WINDOW,
+                "sync": args.sync, "launches": args.warmup + args.steps}
+        fx = next(((n, c) for n, c in tab.items() if all(c["key"].get(k) == v for k, v in want.items())), None)
+    except (OSError, ValueError, KeyError):
+        pass
+    return {"lanes": [L - PRIV_WINDOW, L], "q_sha256": qh, "w_sha256": wh, "launches": args.warmup + args.steps,
+            "fixture": fx[0] if fx else None,
+            "match": (fx[1]["q_sha256"] == qh and fx[1].get("w_sha256") == wh) if fx else None}
+
+
 def counters_for(args, build_id):
     """PMC summary of the dominant kernel for this exact workload, collected from
     this very library (rl_build_id's source hash equal), or None"""
@@ -637,6 +667,8 @@ def main():
                    "global_lanes": world * args.lanes, "train_steps_all_ranks": st_all,
                    "fixture": fx[0] if fx else None,
                    "match": (fx[1]["q_sha256"] == qh and fx[1]["train_steps"] == st_all) if fx else None}
+    elif world == 1 and args.lanes >= PRIV_WINDOW:
+        q_check = private_q_check(args, agent)
     bid = rlamd.build_id()
     pmc = counters_for(args, bid)
     q_repr = agent.q_repr()

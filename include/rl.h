@@ -417,6 +417,11 @@ int rl_agent_peer_attach(rl_agent *a, int32_t rank, int32_t world,
  * 2 peer-read (above) */
 enum rl_merge_path { RL_MERGE_LOCAL = 0, RL_MERGE_RCCL = 1, RL_MERGE_PEER = 2 };
 int rl_agent_merge_path(rl_agent *a, int32_t *path);
+/* ABI 7: private mode, the lanes [lane0, lane0 + n_lanes) only — Q in
+ * rl_agent_get_q's [lane][P][S][A] (NeuralPolicy: get_values, [lane][S][A]) and
+ * the network parameters in rl_agent_get_weights' [lane][n_params] */
+int rl_agent_get_q_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n);
+int rl_agent_get_weights_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n);
 
 /* -------- multi-GPU: the merge as an external collective (shared mode) */
 /* int64 words of the merge buffer the current Q representation uses (all of it)

@@ -1577,7 +1577,15 @@ static double o_delta_bound(const rlo_batch *b) {
     if (!(ep_len * R * 65536.0 < 0x1p50)) return INFINITY;
     return lr * (R + (1.0 + g) * mb);
 }
-static int o_proven(const rlo_batch *b) { return o_delta_bound(b) < 2000.0; }
+/* slippery FrozenLake tables stay f64 under "auto": the fixed point's rounding
+ * flips greedy ties, trajectories part and Q leaves the 1e-5 bar (rl_host.cpp
+ * fix_faithful; tests/golden/longrun.json repr_drift_curve) */
+static int o_faithful(const rlo_batch *b) {
+    return !((b->c.env == RLO_ENV_FROZEN_LAKE || b->c.env == RLO_ENV_FROZEN_LAKE_EDITED) && b->c.slippery);
+}
+static int o_proven(const rlo_batch *b) {
+    return o_delta_bound(b) < 2000.0 && (b->q_forced == RLO_QMODE_FIXED_RANGE || o_faithful(b));
+}
 
 /* representation changes: fixed point -> f64 is exact (|raw| <= 2^51) */
 static void o_to_f64(rlo_batch *b) {
@@ -1589,7 +1597,7 @@ static void o_to_f64(rlo_batch *b) {
 static void o_choose_repr(rlo_batch *b) {
     const size_t nq = (size_t)b->P * b->S * b->A;
     b->qrepr = RLO_QREPR_F64;
-    if (b->priv || b->q_forced || !o_proven(b)) return;
+    if (b->priv || (b->q_forced && b->q_forced != RLO_QMODE_FIXED_RANGE) || !o_proven(b)) return;
     for (size_t k = 0; k < nq; ++k)
         if (!fix_exact(b->qd_base[k])) return;
     for (size_t k = 0; k < nq; ++k) { b->q_base[k] = (int64_t)(b->qd_base[k] * 0x1p40); b->f_base[k] = 0; }
@@ -1769,11 +1777,13 @@ void rlo_batch_set_algo(rlo_batch *b, int32_t algo) {
 /* RLO_QMODE_AUTO: the fixed point where the range proof holds (and the table is
  * exact in it), else f64; RLO_QMODE_F64: f64 always; RLO_QMODE_F64_SEQ (oracle
  * only): f64 with every step / merge sum formed sequentially in lane / group
- * order instead of on the exponent grid — the drift reference */
+ * order instead of on the exponent grid — the drift reference; RLO_QMODE_FIXED_RANGE
+ * (oracle only): the fixed point wherever the range proof holds, slippery maps
+ * included (round 5's "auto": the repr_drift_curve measurement) */
 void rlo_batch_set_q_mode(rlo_batch *b, int mode) {
     if (b->priv) return;
     b->q_forced = mode;
-    if (mode != RLO_QMODE_AUTO) {
+    if (mode != RLO_QMODE_AUTO && mode != RLO_QMODE_FIXED_RANGE) {
         if (b->qrepr == RLO_QREPR_FIXED40) o_to_f64(b);
         return;
     }

@@ -194,7 +194,7 @@ void   rlo_batch_set_reset_step(rlo_batch *b, int on);
 /* shared-Q representation (rlref.c section 2): the int64 fixed point only where
  * the range proof holds, else f64 with the reference's full range */
 enum { RLO_QREPR_FIXED40 = 0, RLO_QREPR_F64 = 1, RLO_QREPR_PRIVATE = 2 };
-enum { RLO_QMODE_AUTO = 0, RLO_QMODE_F64 = 1, RLO_QMODE_F64_SEQ = 2 };
+enum { RLO_QMODE_AUTO = 0, RLO_QMODE_F64 = 1, RLO_QMODE_F64_SEQ = 2, RLO_QMODE_FIXED_RANGE = 3 };
 void   rlo_batch_set_q_mode(rlo_batch *b, int mode);
 int    rlo_batch_q_repr(const rlo_batch *b);
 /* learner groups over every rank (the f64 merge grid's headroom); 0 = local */

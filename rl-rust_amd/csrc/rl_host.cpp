@@ -788,7 +788,18 @@ double delta_bound(const rl_agent *a) {
     if (!(ep_len * R * 65536.0 < 0x1p50)) return inf;
     return lr * emax * (R + (1.0 + g) * mb);
 }
-bool fix_proven(const rl_agent *a) { return delta_bound(a) < 2000.0; }
+// Round 6: on a slippery map the fixed point stays in range
+// but not within the north star's 1e-5 of f64.  Its 2^-40 rounding decides greedy
+// ties the f64 table breaks the other way, lanes' trajectories part from the
+// second launch, and rare transitions then move entries by up to 1.9e-4 (cfg 2
+// slippery, tests/golden/longrun.json repr_drift_curve; the deterministic map stays
+// below 8.5e-6) — so "auto" keeps slippery FrozenLake tables in f64.  Same rule as
+// the oracle's o_proven.
+bool fix_faithful(const rl_agent *a) {
+    const int k = a->cfg.env.kind;
+    return !((k == RL_ENV_FROZEN_LAKE || k == RL_ENV_FROZEN_LAKE_EDITED) && a->cfg.env.slippery);
+}
+bool fix_proven(const rl_agent *a) { return delta_bound(a) < 2000.0 && fix_faithful(a); }
 // The 8-wave kernels pack a step's contributions to an entry into one int64,
 // sum * 2^11 + count (one LDS atomic per contribution instead of two): exact
 // while at most G contributions of at most delta_bound * 2^40 + 1 raw units each
@@ -2555,6 +2566,48 @@ int rl_agent_get_weights(rl_agent *a, double *out, size_t n) {
     HIPC(hipStreamSynchronize(a->stream));
     for (size_t k = 0; k < np; ++k)
         for (size_t l = 0; l < L; ++l) out[l * np + k] = tmp[k * L + l];
+    return RL_OK;
+}
+
+// ABI 7: a window of lanes [lane0, lane0 + n_lanes) of a private-mode agent, in
+// rl_agent_get_q's / rl_agent_get_weights' layouts, without the whole set's copy
+// (2^20 lanes of cfg 7 hold 1.6 GB of Q): the bench's q_check and the full-size tests
+int rl_agent_get_q_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    if (!a->priv) return fail(RL_E_STATE, "shared mode: one merged table (rl_agent_get_q)");
+    if ((uint64_t)lane0 + n_lanes > a->L) return fail(RL_E_ARG, "lane window out of range");
+    const size_t PSA = (size_t)a->P * a->S * a->A;
+    if (n < PSA * n_lanes) return fail(RL_E_ARG, "output too small: need n_lanes*P*S*A");
+    HIPC(hipSetDevice(a->device));
+    if (a->neural) {   // get_values of every state, computed for every lane, the window copied
+        double *d = nullptr;
+        HIPC(hipMalloc(&d, PSA * a->L * 8));
+        launch_net_values(a->kp, d, a->stream);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(out, d + PSA * lane0, PSA * n_lanes * 8, hipMemcpyDeviceToHost, a->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
+        (void)hipFree(d);
+        HIPC(e);
+        return RL_OK;
+    }
+    HIPC(hipMemcpyAsync(out, a->q_priv + PSA * lane0, PSA * n_lanes * 8, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    return RL_OK;
+}
+int rl_agent_get_weights_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n) {
+    if (!a || !out) return fail(RL_E_ARG, "null argument");
+    if (!a->neural) return fail(RL_E_STATE, "not a NeuralPolicy agent");
+    if ((uint64_t)lane0 + n_lanes > a->L) return fail(RL_E_ARG, "lane window out of range");
+    const size_t np = a->n_params, L = a->L;
+    if (n < np * n_lanes) return fail(RL_E_ARG, "output too small: need n_lanes*n_params");
+    HIPC(hipSetDevice(a->device));
+    std::vector<double> tmp(np * n_lanes);   // device [param][lane]: one strided copy
+    HIPC(hipMemcpy2DAsync(tmp.data(), (size_t)n_lanes * 8, a->net_w + lane0, L * 8, (size_t)n_lanes * 8, np,
+                          hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (size_t k = 0; k < np; ++k)
+        for (size_t l = 0; l < n_lanes; ++l) out[l * np + k] = tmp[k * n_lanes + l];
     return RL_OK;
 }
 

@@ -161,6 +161,8 @@ SIGNATURES = {
     "rl_agent_peer_handle": (C.c_int, [_V, _V]),
     "rl_agent_peer_attach": (C.c_int, [_V, C.c_int32, C.c_int32, _V]),
     "rl_agent_merge_path": (C.c_int, [_V, _P(C.c_int32)]),
+    "rl_agent_get_q_lanes": (C.c_int, [_V, C.c_uint32, C.c_uint32, _V, C.c_size_t]),
+    "rl_agent_get_weights_lanes": (C.c_int, [_V, C.c_uint32, C.c_uint32, _V, C.c_size_t]),
 }
 PEER_HANDLE_BYTES = 64
 MERGE_PATHS = {0: "local", 1: "rccl", 2: "peer"}
@@ -592,6 +594,18 @@ class Agent:
         assert len(handles) == world and all(len(h) == PEER_HANDLE_BYTES for h in handles)
         buf = (C.c_uint8 * (PEER_HANDLE_BYTES * world)).from_buffer_copy(b"".join(handles))
         check(lib().rl_agent_peer_attach(self.h, rank, world, buf))
+
+    def q_lanes(self, lane0, n_lanes):
+        """private mode: Q of lanes [lane0, lane0 + n_lanes), [n][P][S][A] as q()'s"""
+        q = np.zeros((n_lanes, self.P, self.S, self.A), np.float64)
+        check(lib().rl_agent_get_q_lanes(self.h, lane0, n_lanes, q.ctypes.data, q.size))
+        return q
+
+    def weights_lanes(self, lane0, n_lanes):
+        nin, hid, npar = self.net_dims()
+        w = np.zeros((n_lanes, npar), np.float64)
+        check(lib().rl_agent_get_weights_lanes(self.h, lane0, n_lanes, w.ctypes.data, w.size))
+        return w
 
     def merge_path(self):
         v = C.c_int32()

@@ -78,14 +78,18 @@ def case(name):
     return name, out
 
 
-def generate(workers=5):
+def generate(workers=5, only=None, old=None):
+    names = [k for k in CASES if only is None or k in only]
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        res = dict(ex.map(case, list(CASES)))
+        res = dict(ex.map(case, names))
     return {"source": "tests/golden/make_fullsize.py (oracle/rlref.c batched schedule, seed 0x5EED)",
-            **{k: res[k] for k in CASES}}
+            **{k: res[k] if k in res else old[k] for k in CASES if k in res or (old and k in old)}}
 
 
 if __name__ == "__main__":
+    # python make_fullsize.py [name ...]: regenerate only these cases, keep the others
     path = os.path.join(HERE, "fullsize.json")
-    json.dump(generate(), open(path, "w"), indent=1)
+    only = sys.argv[1:] or None
+    old = json.load(open(path)) if only else None
+    json.dump(generate(only=only, old=old), open(path, "w"), indent=1)
     print("wrote", path, os.path.getsize(path), "bytes")

@@ -47,7 +47,7 @@ RECORD_DTYPE = np.dtype([("s", "<u4"), ("s2", "<u4"), ("a", "u1"), ("a2", "u1"),
 KIND_IDLE, KIND_RESET, KIND_STEP, KIND_RESET_STEP = 0, 1, 2, 3
 # shared-Q representation (oracle/rlref.h): reported / requested
 QREPR = {0: "fixed40", 1: "f64", 2: "private"}
-QMODE = {"auto": 0, "f64": 1, "f64_seq": 2}
+QMODE = {"auto": 0, "f64": 1, "f64_seq": 2, "fixed_range": 3}
 assert RECORD_DTYPE.itemsize == 32
 
 
@@ -461,8 +461,10 @@ class Batch:
         return out.reshape(-1, self.L)
 
     def set_q_mode(self, mode):
-        """'auto' (fixed point where proven), 'f64', or 'f64_seq' (oracle only: f64
-        with sequential lane-order / group-order sums, the drift reference)"""
+        """'auto' (fixed point where proven), 'f64', 'f64_seq' (oracle only: f64
+        with sequential lane-order / group-order sums, the drift reference) or
+        'fixed_range' (oracle only: the fixed point wherever the range proof holds,
+        slippery maps included — round 5's auto, for the drift curve)"""
         lib().rlo_batch_set_q_mode(self.h, QMODE[mode])
 
     def q_repr(self):

@@ -30,6 +30,7 @@ REPR_CASES = [
     (dict(env="cliff_walking", agent="traces", algo="sarsa"), "f64"),
     (dict(env="taxi", selector="ucb", algo="expected_sarsa"), "f64"),
     (dict(env="frozen_lake", algo="qlearning", gamma=1.0), "f64"),
+    (dict(env="frozen_lake", map8x8=1, slippery=1, algo="qlearning"), "f64"),   # round 6: fix_faithful
 ]
 
 

@@ -112,12 +112,21 @@ def test_set_q_representations_and_blackjack_terminal_rows(oracle):
     (dict(env="cliff_walking", agent="traces", algo="sarsa"), "f64"),
     (dict(env="taxi", selector="ucb", algo="expected_sarsa"), "f64"),
     (dict(env="frozen_lake", algo="qlearning", gamma=1.0), "f64"),
-], ids=["fl-q", "taxi-es", "cw-ucb-sarsa", "bj-double", "cw-traces", "taxi-ucb-es", "gamma1"])
+    (dict(env="frozen_lake", map8x8=1, slippery=1, algo="qlearning"), "f64"),
+    (dict(env="frozen_lake_edited", slippery=1, algo="sarsa"), "f64"),
+], ids=["fl-q", "taxi-es", "cw-ucb-sarsa", "bj-double", "cw-traces", "taxi-ucb-es", "gamma1", "fl-slippery",
+        "fle-slippery"])
 def test_representation_follows_the_range_proof(oracle, kw, want):
     """The fixed point only where the proof holds (one-step, single table,
-    contracting bootstrap: rlref.c o_delta_bound), f64 everywhere else."""
+    contracting bootstrap: rlref.c o_delta_bound) and on deterministic maps (round
+    6: slippery FrozenLake leaves 1e-5 of f64, longrun.json repr_drift_curve), f64
+    everywhere else; 'fixed_range' (oracle only) is round 5's rule without the map
+    condition."""
     b = oracle.Batch(oracle.default_params(n_lanes=64, group_size=32, **kw))
     assert b.q_repr() == want
+    if kw.get("slippery"):
+        b.set_q_mode("fixed_range")
+        assert b.q_repr() == "fixed40"
 
 
 def test_representation_changes(oracle):
