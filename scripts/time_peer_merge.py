@@ -1,5 +1,5 @@
-"""World-2 latency of the one-shot peer-read merge (rl.h ABI 7):
-two ranks sharing the box's one GPU (RCCL refuses two ranks on one device, so the
+"""Latency of the one-shot peer-read merge (rl.h ABI 7) at
+world 2 (PEER_RANKS=4: four): the ranks sharing the box's one GPU (RCCL refuses two ranks on one device, so the
 handles travel over gloo), each with bench.py's agent for a workload's per-rank
 shard, time on the agent's stream with HIP events
   - the merge alone (rl_agent_sync: [MAX peer reduce] -> fold -> SUM peer reduce
@@ -9,7 +9,7 @@ beside the same agent's merge with no peers (fold / apply only).  Both ranks iss
 their merges back to back, so a peer-read merge's time includes waiting for the
 other rank's flag; scripts/time_merge.py gives RCCL's world-1 figure.
 
-    python scripts/time_peer_merge.py [cfg[:lanes_per_rank] ...]   (GPU; rank 0 prints one JSON line per case)
+    [PEER_RANKS=4] python scripts/time_peer_merge.py [cfg[:lanes_per_rank] ...]   (GPU; rank 0 prints one JSON line per case)
 """
 import json
 import os
@@ -22,14 +22,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = 200
 
 
-def spawn(argv):
+def spawn(argv, n):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
-                              env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                                       MASTER_PORT=str(port)), cwd=ROOT) for r in range(2)]
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                                       MASTER_PORT=str(port)), cwd=ROOT) for r in range(n)]
     rc = 0
     for p in procs:
         try:
@@ -63,7 +63,10 @@ def rank_main(argv):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / n
 
-    for c in argv or ["2:131072", "2:524288", "4:131072", "5:262144", "3:524288"]:
+    cases = argv or ["2:131072", "2:524288", "4:131072", "5:262144", "3:524288"]
+    # the first case once more ahead, not printed: the ranks' start-up (other
+    # processes still loading, first launches) inflated the first case's timings
+    for i, c in enumerate([cases[0]] + cases):
         cf, _, ln = c.partition(":")
         kw = bench_params(int(cf), {"n_lanes": int(ln)} if ln else {})
         L = kw["n_lanes"]
@@ -82,11 +85,12 @@ def rank_main(argv):
         a.peer_attach(rank, world, hs)
         a.set_merge_groups(world * ((L + kw["group_size"] - 1) // kw["group_size"]))
         assert a.merge_path() == "peer"
-        out["merge_peer_w2_ms"] = timed(s, a.sync)
-        out["run_launch_peer_w2_ms"] = timed(s, lambda: a.run(1), 32)
+        timed(s, a.sync, 20)     # warm: both ranks' first merges (code objects, IPC mappings)
+        out["merge_peer_ms"] = timed(s, a.sync)
+        out["run_launch_peer_ms"] = timed(s, lambda: a.run(1), 32)
         a.synchronize()      # raises if a peer wait timed out
         a.close()
-        if rank == 0:
+        if rank == 0 and i > 0:
             print(json.dumps(out), flush=True)
         dist.barrier()
     dist.destroy_process_group()
@@ -96,4 +100,4 @@ if __name__ == "__main__":
     if "RANK" in os.environ:
         rank_main(sys.argv[1:])
     else:
-        sys.exit(spawn(sys.argv[1:]))
+        sys.exit(spawn(sys.argv[1:], int(os.environ.get("PEER_RANKS", "2"))))

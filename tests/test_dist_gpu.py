@@ -85,6 +85,22 @@ def test_two_rank_peer_merge_equals_one_process(tmp_path, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["fl8x8-qlearning", "blackjack-double-q"])
+def test_four_rank_peer_merge_equals_one_process(tmp_path, name):
+    """The peer-read merge with four ranks (four processes sharing the GPU): every
+    rank waits for three peers' flags and sums four regions in rank order — the
+    N > 2 logic the driver's 8-GPU runs take — and still ends with one process's Q"""
+    case = dict(CASES[name], sync_every=32, n_launch=3, lanes_per_rank=4096, merge="peer", train_episodes=2)
+    out = tmp_path / "res.json"
+    r = _torchrun([os.path.join("tests", "dist_gpu_worker.py"), str(out), json.dumps(case)], n=4, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.load(open(out))
+    assert res["merge_path"] == "peer", res
+    assert res["steps_ranks"] == res["steps_one"] > 0, res
+    assert res["q_equal"] and res["qf_equal"], res
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_prints_one_line():
     r = _torchrun(["bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1", "--lanes", str(1 << 16),
                    "--no-cpu-baseline"])
