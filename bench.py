@@ -395,6 +395,15 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     rows = 484 if (args.env == "blackjack" and args.selector != "ucb") else agent.S   # LDS rows per group
     slot_bytes = 8 * agent.P * rows * agent.A * groups if agent.q_repr() == "f64" else 0
     fused_bytes = 2 * 56 * lanes + slot_bytes
+    # traces (shared): the lanes' eligibility-trace sets outlive a launch as the lane
+    # records do — read in and written out once per launch: 10 B per visited pair
+    # (u16 id + f64 E; the whole-row layout of UCB + expected SARSA: A x 8 B + a
+    # 2 B list entry per visited state); their count at the run's end
+    # (rl_agent_trace_items) stands for the launch boundaries'
+    trace_items = agent.trace_items() if (args.agent == "traces" and args.group != 1) else 0
+    if trace_items:
+        pairs = not (args.selector == "ucb" and args.algo == "expected_sarsa")
+        fused_bytes += 2 * (10 if pairs else 8 * n_act + 2) * trace_items
     kname = "k_train_private" if args.group == 1 else "k_train_shared"
     basis_priv = ("private agents: 2 x 56 B lane record per lane per launch + per env-step the lane's own "
                   "table traffic (tabular: row s2, Q(s,a) read + written, x (1 + planning steps); neural: "
@@ -438,9 +447,12 @@ def roofline(args, agent, steps_done, avg_kern_s, pmc):
     out = {"kernel": kname, "kernel_avg_ms": avg_kern_s * 1e3,
            "hbm": {"fused_bytes_per_launch": fused_bytes, "fused_frac": fused_frac,
                    "fused_basis": ("2 x 56 B lane record per lane per launch (+ 8 B x LDS entries per group "
-                                   "for f64 tables): the fused kernel keeps lanes in registers for K steps")
+                                   "for f64 tables; traces: + 2 x 10 B per live trace pair, in and out once): the "
+                                   "fused kernel keeps lanes in registers for K steps")
                    if args.group != 1 else basis_priv,
+                   **({"trace_items": trace_items} if trace_items else {}),
                    "traffic_bytes_per_launch": traffic, "traffic_frac": traffic_frac,
+                   "traffic_over_fused": (traffic / fused_bytes) if traffic else None,
                    "peak_GBps": HBM_PEAK / 1e9},
            "hbm_priced": {"bytes_per_env_step": bytes_per_step, "GBps_equiv": priced / 1e9,
                           "ratio_to_peak": priced / HBM_PEAK,

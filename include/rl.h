@@ -422,6 +422,9 @@ int rl_agent_merge_path(rl_agent *a, int32_t *path);
  * the network parameters in rl_agent_get_weights' [lane][n_params] */
 int rl_agent_get_q_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n);
 int rl_agent_get_weights_lanes(rl_agent *a, uint32_t lane0, uint32_t n_lanes, double *out, size_t n);
+/* ABI 7: live eligibility-trace entries over every lane (the visited pairs of the
+ * shared pair layout, visited states otherwise); 0 without traces */
+int rl_agent_trace_items(rl_agent *a, uint64_t *items);
 
 /* -------- multi-GPU: the merge as an external collective (shared mode) */
 /* int64 words of the merge buffer the current Q representation uses (all of it)

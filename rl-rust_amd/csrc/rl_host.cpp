@@ -1739,6 +1739,23 @@ int rl_agent_lane_state(rl_agent *a, uint32_t *core, uint32_t *aux, size_t n) {
     return RL_OK;
 }
 
+// ABI 7: the live eligibility-trace entries of every lane (shared pair layout: the
+// pairs of the lanes' visited sets — a pool keeps its wave's count at the wave's
+// first lane; row layout / private: visited states) at the call.  They persist
+// across launches like the lane records: each launch reads them in and writes them
+// out once (bench.py's algorithmic bytes for the traces rows)
+int rl_agent_trace_items(rl_agent *a, uint64_t *items) {
+    if (!a || !items) return fail(RL_E_ARG, "null argument");
+    *items = 0;
+    if (!a->tcnt) return RL_OK;
+    HIPC(hipSetDevice(a->device));
+    std::vector<uint32_t> t(a->L);
+    HIPC(hipMemcpyAsync(t.data(), a->tcnt, (size_t)a->L * 4, hipMemcpyDeviceToHost, a->stream));
+    HIPC(hipStreamSynchronize(a->stream));
+    for (uint32_t v : t) *items += v;
+    return RL_OK;
+}
+
 int rl_agent_get_q(rl_agent *a, double *out, size_t n) {
     if (!a || !out) return fail(RL_E_ARG, "null argument");
     HIPC(hipSetDevice(a->device));

@@ -163,6 +163,7 @@ SIGNATURES = {
     "rl_agent_merge_path": (C.c_int, [_V, _P(C.c_int32)]),
     "rl_agent_get_q_lanes": (C.c_int, [_V, C.c_uint32, C.c_uint32, _V, C.c_size_t]),
     "rl_agent_get_weights_lanes": (C.c_int, [_V, C.c_uint32, C.c_uint32, _V, C.c_size_t]),
+    "rl_agent_trace_items": (C.c_int, [_V, _P(C.c_uint64)]),
 }
 PEER_HANDLE_BYTES = 64
 MERGE_PATHS = {0: "local", 1: "rccl", 2: "peer"}
@@ -606,6 +607,11 @@ class Agent:
         w = np.zeros((n_lanes, npar), np.float64)
         check(lib().rl_agent_get_weights_lanes(self.h, lane0, n_lanes, w.ctypes.data, w.size))
         return w
+
+    def trace_items(self):
+        v = C.c_uint64()
+        check(lib().rl_agent_trace_items(self.h, C.byref(v)))
+        return v.value
 
     def merge_path(self):
         v = C.c_int32()

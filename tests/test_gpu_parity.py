@@ -445,6 +445,26 @@ def test_pair_trace_lds_slots(rl, oracle, trc_kb, monkeypatch):
     _assert_stats_equal(dev, ref)
 
 
+def test_trace_items_count_live_pairs(rl):
+    """rl_agent_trace_items (ABI 7): the live trace entries bench.py's algorithmic
+    bytes count — 0 before any step, bounded by every lane's S*A pairs, non-zero
+    while episodes are open, and 0 again after train() (every episode ends and
+    the sets are cleared: elegibility_traces_agent.rs:98-100)"""
+    for kw in (dict(env="cliff_walking", group_size=256), dict(env="taxi", group_size=64)):
+        p = rl.default_params(agent="traces", algo="sarsa", n_lanes=4096, sync_every=16, **kw)
+        a = rl.Agent(p)
+        assert a.trace_items() == 0
+        a.run(3)
+        n = a.trace_items()
+        assert 0 < n <= 4096 * a.S * a.A, n
+        a.train(1, 0)
+        assert a.trace_items() == 0
+        a.close()
+    one = rl.Agent(rl.default_params(n_lanes=64, group_size=64))
+    one.run(1)
+    assert one.trace_items() == 0
+
+
 @pytest.mark.parametrize("env", ["taxi", "blackjack"])
 def test_pair_trace_cap_change_mid_episode(rl, oracle, env, monkeypatch):
     """a lane's pair list outlives the launch (p.tcnt) while its LDS
