@@ -408,7 +408,9 @@ int rl_agent_sync(rl_agent *a);
  * RCCL refuses two ranks) the caller exchanges the handles:
  *   rl_agent_peer_handle on every rank -> all-gather them (rank order) ->
  *   rl_agent_peer_attach on every rank; then rl_agent_run / train / evaluate /
- *   rl_agent_sync merge over the peers.  Every rank must make the same merges. */
+ *   rl_agent_sync merge over the peers.  Every rank must make the same merges, and
+ *   destroy its agent only after every rank's last merge is complete (a barrier
+ *   after rl_agent_synchronize): a peer may still be reading its region. */
 #define RL_PEER_HANDLE_BYTES 64
 int rl_agent_peer_handle(rl_agent *a, void *handle_out /* RL_PEER_HANDLE_BYTES */);
 int rl_agent_peer_attach(rl_agent *a, int32_t rank, int32_t world,
