@@ -2319,7 +2319,11 @@ int rl_agent_set_comm(rl_agent *a, rl_comm *c) {
     a->merge_groups = total;
     a->merge_groups_set = c != nullptr;
     const char *mp = getenv("RLAMD_MERGE");
-    if (c && c->world > 1 && !(mp && !strcmp(mp, "rccl"))) return comm_peer_setup(a);
+    // RLAMD_PEER_WORLD1=1 (tests): the whole setup — the handles' all-gather over RCCL,
+    // the agreement, the self-test — and the peer merges at world 1 too, so the box's
+    // one GPU runs the path the driver's N-GPU runs take
+    const bool w1 = getenv("RLAMD_PEER_WORLD1") != nullptr;
+    if (c && (c->world > 1 || w1) && !(mp && !strcmp(mp, "rccl"))) return comm_peer_setup(a);
     return RL_OK;
 }
 
@@ -2458,7 +2462,7 @@ int rl_agent_peer_attach(rl_agent *a, int32_t rank, int32_t world, const void *h
     }
     HIPC(hipMemset(pm.err_d, 0, 4));
     pm.epoch = 0;
-    pm.on = world > 1;
+    pm.on = world > 1 || getenv("RLAMD_PEER_WORLD1") != nullptr;
     return RL_OK;
 }
 

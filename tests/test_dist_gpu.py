@@ -190,3 +190,22 @@ def test_bench_gpus2_peer_merge_q_check(config, fixture):
     qc = d["q_check"]
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["merge_path"] == "peer", d["config"]
     assert qc["ranks_agree"] is True and qc["fixture"] == fixture and qc["match"] is True, json.dumps(qc)
+
+
+@pytest.mark.gpu
+def test_bench_rccl_peer_setup_one_rank():
+    """bench.py's driver path at N > 1 — librlamd's RCCL communicator, then the
+    peer-read setup inside rl_agent_set_comm (handles all-gathered over RCCL,
+    agreement, self-test) — run at one rank (RLAMD_PEER_WORLD1: the box has one
+    GPU): every merge through the peer kernels, and the driver-shape run's merged Q
+    the oracle's (q_check cfg2_L1M_25)"""
+    env = dict(os.environ, RLAMD_FORCE_COMM="1", RLAMD_PEER_WORLD1="1", MASTER_ADDR="127.0.0.1")
+    env.pop("RLAMD_COLLECTIVE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--steps", "20",
+           "--warmup", "5", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    assert d["config"]["merge_path"] == "peer", d["config"]
+    assert d["q_check"]["fixture"] == "cfg2_L1M_25" and d["q_check"]["match"] is True, d["q_check"]

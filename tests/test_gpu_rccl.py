@@ -64,3 +64,32 @@ def test_comm_rejects_private_mode(rl, comm):
     a = rl.Agent(rl.default_params(env="frozen_lake", n_lanes=8, group_size=1))
     with pytest.raises(rl.RLError):
         a.set_comm(comm)
+
+
+@pytest.mark.parametrize("case", CASES, ids=["fl", "taxi-ucb-es", "cw-traces", "bj-double"])
+def test_comm_peer_setup_world1(rl, oracle, case, monkeypatch):
+    """rl_agent_set_comm's peer-read setup as the driver's N-GPU runs take it —
+    the exchange handles all-gathered over RCCL (in place), the agreement, the
+    self-test merge of known sums and maxima — run at world 1 (RLAMD_PEER_WORLD1:
+    the box has one GPU), and every later merge of run() and train() through the
+    peer kernels: bit-exact against the oracle"""
+    monkeypatch.setenv("RLAMD_PEER_WORLD1", "1")
+    c = rl.Comm(0, 1, rl.comm_unique_id(), 0)
+    try:
+        p = rl.default_params(n_lanes=3000, sync_every=16, n_episodes_for_decay=40, **case)
+        a = rl.Agent(p)
+        a.set_comm(c)
+        assert a.merge_path() == "peer"
+        a.run(5)
+        a.train(4, 2)
+        a.synchronize()
+        ref = oracle.Batch(p)
+        ref.run(5)
+        ref.train_episodes(4, 2)
+        assert np.array_equal(a.q_raw(), ref.q_raw())
+        _assert_stats_equal(a, ref)
+        a.set_comm(None)
+        assert a.merge_path() == "local"
+        a.close()
+    finally:
+        c.close()
