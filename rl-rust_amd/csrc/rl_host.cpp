@@ -973,6 +973,19 @@ int launch_train_kernel(rl_agent *a, bool *merge = nullptr) {
                    !a->peer.on) {
             launch_fold_apply(a->kp, a->stream);   // fold the replicas and apply (eps-greedy: sums + counts only)
             *merge = true;
+        } else if (merge && a->peer.on) {
+            // the fixed point over the peers: the replicas folded into this rank's
+            // exchange slot, then the ranks' words reduced and applied (two launches)
+            auto &pm = a->peer;
+            uint64_t mw, sw;
+            merge_layout(a, &mw, &sw);
+            if (sw > pm.cap) return fail(RL_E_STATE, "merge buffer larger than the peer exchange slots");
+            const uint64_t slot = (uint64_t)(pm.epoch & 1) * pm.cap;
+            ++pm.epoch;
+            launch_peer_fold_put(a->kp, pm.region + slot, a->stream);
+            launch_peer_reduce_apply(a->kp, pm.bases_d, (uint32_t)pm.world, (uint32_t)pm.rank, slot,
+                                     2 * pm.cap + 16, pm.epoch, pm.err_d, pm.timeout_ticks, a->stream);
+            *merge = true;
         } else {
             launch_fold_replicas(a->kp, a->stream);   // fold the group-delta replicas into the delta
         }

@@ -192,6 +192,11 @@ void launch_peer_put(const int64_t *src, int64_t *slot, uint64_t n, hipStream_t 
 void launch_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank, uint64_t slot_off, uint64_t flag_off,
                         uint64_t n, int64_t epoch, int op_max, int64_t *dst, uint32_t *err, int64_t timeout_ticks,
                         hipStream_t s);
+// the fixed point's merge over the peers in two launches (fold into the slot; reduce + apply)
+void launch_peer_fold_put(const KParams &p, int64_t *slot, hipStream_t s);
+void launch_peer_reduce_apply(const KParams &p, int64_t *const *bases, uint32_t world, uint32_t rank,
+                              uint64_t slot_off, uint64_t flag_off, int64_t epoch, uint32_t *err,
+                              int64_t timeout_ticks, hipStream_t s);
 
 // env-only kernels (batched Env trait) and KAT probes
 void launch_env_reset(int env, const KParams &p, hipStream_t s, uint64_t *obs);

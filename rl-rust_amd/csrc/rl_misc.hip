@@ -171,10 +171,12 @@ __global__ void k_peer_put(const int64_t *src, int64_t *slot, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) __hip_atomic_store(&slot[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ void __launch_bounds__(256) k_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank,
-                                                     uint64_t slot_off, uint64_t flag_off, uint64_t n,
-                                                     int64_t epoch, int32_t op_max, int64_t *dst, uint32_t *err,
-                                                     int64_t timeout_ticks) {
+// block 0 raises this rank's flag to `epoch`; every block waits until each peer's
+// flag is >= epoch (or the wall clock passes timeout_ticks: *err set).  Every
+// thread of the block calls it (one barrier); true when the peers arrived
+__device__ __forceinline__ bool peer_arrive_wait(int64_t *const *bases, uint32_t world, uint32_t rank,
+                                                 uint64_t flag_off, int64_t epoch, uint32_t *err,
+                                                 int64_t timeout_ticks) {
     __shared__ uint32_t timed_out;
     if (threadIdx.x == 0) {
         timed_out = 0u;
@@ -194,8 +196,15 @@ __global__ void __launch_bounds__(256) k_peer_reduce(int64_t *const *bases, uint
         }
     }
     __syncthreads();
+    return timed_out == 0u;
+}
+__global__ void __launch_bounds__(256) k_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank,
+                                                     uint64_t slot_off, uint64_t flag_off, uint64_t n,
+                                                     int64_t epoch, int32_t op_max, int64_t *dst, uint32_t *err,
+                                                     int64_t timeout_ticks) {
+    const bool ok = peer_arrive_wait(bases, world, rank, flag_off, epoch, err, timeout_ticks);
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (timed_out || i >= n) return;
+    if (!ok || i >= n) return;
     int64_t acc = op_max ? INT64_MIN : 0;
     for (uint32_t r = 0; r < world; ++r) {
         const int64_t v = __hip_atomic_load(&bases[r][slot_off + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -212,6 +221,61 @@ void launch_peer_reduce(int64_t *const *bases, uint32_t world, uint32_t rank, ui
     // at least one block: block 0 raises the flag even for n == 0
     hipLaunchKernelGGL(k_peer_reduce, dim3((unsigned)(n ? (n + 255) / 256 : 1)), dim3(256), 0, s,
                        bases, world, rank, slot_off, flag_off, n, epoch, op_max, dst, err, timeout_ticks);
+}
+
+// The fixed-point merge over the peers in two launches instead of four (round 6):
+// the replicas folded straight into this rank's exchange slot (k_peer_fold_put:
+// k_fold_replicas' sum written with system-scope stores), then the N ranks' words
+// reduced and applied in one pass (k_peer_reduce_apply: k_apply's rule on the
+// rank-order sums — Q_base += mean_delta(Σ dQ, Σ counts), N / t += Σ Δ).
+__global__ void __launch_bounds__(256) k_peer_fold_put(KParams p, int64_t *slot) {
+    __shared__ uint64_t part[4][64];
+    const uint32_t lw = threadIdx.x & 63u, g = threadIdx.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * 64u + lw;
+    uint64_t s = 0;
+    if (w < p.sum_words) {
+        int64_t *x = p.delta_rep + (uint64_t)g * p.delta_words + w;
+        const uint64_t stride = 4ull * p.delta_words;
+        const uint32_t n = p.n_rep > g ? (p.n_rep - g + 3u) / 4u : 0u;
+#pragma unroll 16
+        for (uint32_t i = 0; i < n; ++i) s += (uint64_t)x[i * stride];
+#pragma unroll 16
+        for (uint32_t i = 0; i < n; ++i) x[i * stride] = 0;
+    }
+    part[g][lw] = s;
+    __syncthreads();
+    if (g == 0 && w < p.sum_words) {
+        const int64_t v = (int64_t)((uint64_t)p.delta[w] + part[0][lw] + part[1][lw] + part[2][lw] + part[3][lw]);
+        __hip_atomic_store(&slot[w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        p.delta[w] = 0;
+    }
+}
+__global__ void __launch_bounds__(256) k_peer_reduce_apply(KParams p, int64_t *const *bases, uint32_t world,
+                                                           uint32_t rank, uint64_t slot_off, uint64_t flag_off,
+                                                           int64_t epoch, uint32_t *err, int64_t timeout_ticks) {
+    const bool ok = peer_arrive_wait(bases, world, rank, flag_off, epoch, err, timeout_ticks);
+    const uint32_t PSA = p.P * p.S * p.A, SA = p.S * p.A;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!ok) return;
+    auto rsum = [&](uint64_t w) -> int64_t {   // the ranks' words in rank order (exact)
+        uint64_t acc = 0;
+        for (uint32_t r = 0; r < world; ++r)
+            acc += (uint64_t)__hip_atomic_load(&bases[r][slot_off + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return (int64_t)acc;
+    };
+    if (i < PSA) p.q_base[i] = p.q_base[i] + mean_delta(rsum(i), rsum(PSA + i));
+    if (i < SA) p.n_base[i] = p.n_base[i] + (uint64_t)rsum(2ull * PSA + i);
+    if (i == 0) p.t_base[0] = (uint64_t)((int64_t)p.t_base[0] + rsum(2ull * PSA + SA));
+}
+void launch_peer_fold_put(const KParams &p, int64_t *slot, hipStream_t s) {
+    hipLaunchKernelGGL(k_peer_fold_put, dim3((p.sum_words + 63) / 64), dim3(256), 0, s, p, slot);
+}
+void launch_peer_reduce_apply(const KParams &p, int64_t *const *bases, uint32_t world, uint32_t rank,
+                              uint64_t slot_off, uint64_t flag_off, int64_t epoch, uint32_t *err,
+                              int64_t timeout_ticks, hipStream_t s) {
+    const uint32_t PSA = p.P * p.S * p.A;
+    hipLaunchKernelGGL(k_peer_reduce_apply, dim3((PSA + 255) / 256), dim3(256), 0, s, p, bases, world, rank,
+                       slot_off, flag_off, epoch, err, timeout_ticks);
 }
 
 // ---------------------------------------------------------------- replica fold

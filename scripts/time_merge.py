@@ -4,7 +4,8 @@ bench.py's geometry, time on the agent's stream with HIP events
   - the merge after it (rl_agent_sync: [MAX all-reduce] -> fold -> SUM
     all-reduce -> apply) with a world-1 RCCL communicator attached,
   - the same merge without a communicator (fold / apply kernels only),
-and the host time of the train()/evaluate() loop per launch.  The difference
+the same through the peer-read path at world 1 (RLAMD_PEER_WORLD1), and the host
+time of the train()/evaluate() loop per launch.  The difference
 of the two merge timings is RCCL's fixed cost at world 1; DESIGN.md §6 projects
 8 ranks from it.
 
@@ -59,6 +60,15 @@ def one(cfg, lanes=None):
     a.set_comm(comm)
     out["merge_rccl_w1_ms"], out["merge_rccl_w1_host_ms"] = timed(s, a.sync)
     out["run_launch_rccl_w1_ms"], _ = timed(s, lambda: a.run(1), 32)
+    # the peer-read path at world 1 (RLAMD_PEER_WORLD1: set_comm's setup, then every
+    # merge through the peer kernels; run(1) takes the fixed point's fused pair)
+    os.environ["RLAMD_PEER_WORLD1"] = "1"
+    a.set_comm(comm)
+    assert a.merge_path() == "peer"
+    out["merge_peer_w1_ms"], _ = timed(s, a.sync)
+    out["run_launch_peer_w1_ms"], _ = timed(s, lambda: a.run(1), 32)
+    del os.environ["RLAMD_PEER_WORLD1"]
+    a.set_comm(comm)
     for tag, comm_on in (("rccl_w1", True), ("local", False)):
         a.set_comm(comm if comm_on else None)
         l0 = a.stats()["launches"]
