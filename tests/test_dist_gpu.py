@@ -85,7 +85,7 @@ def test_two_rank_peer_merge_equals_one_process(tmp_path, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["fl8x8-qlearning", "blackjack-double-q"])
+@pytest.mark.parametrize("name", list(CASES))
 def test_four_rank_peer_merge_equals_one_process(tmp_path, name):
     """The peer-read merge with four ranks (four processes sharing the GPU): every
     rank waits for three peers' flags and sums four regions in rank order — the
@@ -98,6 +98,8 @@ def test_four_rank_peer_merge_equals_one_process(tmp_path, name):
     assert res["merge_path"] == "peer", res
     assert res["steps_ranks"] == res["steps_one"] > 0, res
     assert res["q_equal"] and res["qf_equal"], res
+    if "ucb_equal" in res:
+        assert res["ucb_equal"], res
 
 
 @pytest.mark.gpu
