@@ -175,22 +175,24 @@ def test_bench_gpus2_self_launch_strong_default():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config,fixture", [(2, "cfg2_L1M_25"), (4, "cfg4_L512K_25")], ids=["cfg2", "cfg4"])
-def test_bench_gpus2_peer_merge_q_check(config, fixture):
-    """`bench.py --gpus 2` (self-launched ranks sharing the
+@pytest.mark.parametrize("config,fixture,n", [(2, "cfg2_L1M_25", 2), (4, "cfg4_L512K_25", 2),
+                                              (4, "cfg4_L512K_25", 4)], ids=["cfg2", "cfg4", "cfg4-4ranks"])
+def test_bench_gpus2_peer_merge_q_check(config, fixture, n):
+    """`bench.py --gpus N` (self-launched ranks sharing the
     GPU) with the one-shot peer-read merge in every launch: the default strong split
-    of BASELINE's global lane set (cfg 2: 2^20; cfg 4: 2^19, "2^19 envs, 4xMI355X")
-    ends with the oracle's one-process Q for that set over the driver's 25 launches"""
+    of BASELINE's global lane set (cfg 2: 2^20; cfg 4: 2^19, "2^19 envs, 4xMI355X" —
+    also at its 4 ranks) ends with the oracle's one-process Q for that set over the
+    driver's 25 launches"""
     env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", RLAMD_COLLECTIVE="peer")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, "bench.py", "--config", str(config), "--gpus", "2", "--steps", "20",
+    r = subprocess.run([sys.executable, "bench.py", "--config", str(config), "--gpus", str(n), "--steps", "20",
                         "--warmup", "5", "--no-cpu-baseline"], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     d = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
     qc = d["q_check"]
-    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["merge_path"] == "peer", d["config"]
+    assert d["n_gpus"] == n and d["scaling"] == "strong" and d["config"]["merge_path"] == "peer", d["config"]
     assert qc["ranks_agree"] is True and qc["fixture"] == fixture and qc["match"] is True, json.dumps(qc)
 
 
