@@ -176,13 +176,16 @@ def test_bench_gpus2_self_launch_strong_default():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("config,fixture,n", [(2, "cfg2_L1M_25", 2), (4, "cfg4_L512K_25", 2),
-                                              (4, "cfg4_L512K_25", 4)], ids=["cfg2", "cfg4", "cfg4-4ranks"])
+                                              (4, "cfg4_L512K_25", 4), (2, "cfg2_L1M_25", 8),
+                                              (5, "cfg5_L4M_25", 8)],
+                         ids=["cfg2", "cfg4", "cfg4-4ranks", "cfg2-8ranks", "cfg5-8ranks"])
 def test_bench_gpus2_peer_merge_q_check(config, fixture, n):
     """`bench.py --gpus N` (self-launched ranks sharing the
     GPU) with the one-shot peer-read merge in every launch: the default strong split
     of BASELINE's global lane set (cfg 2: 2^20; cfg 4: 2^19, "2^19 envs, 4xMI355X" —
-    also at its 4 ranks) ends with the oracle's one-process Q for that set over the
-    driver's 25 launches"""
+    also at its 4 ranks; cfg 2 and cfg 5's "2^22 envs across 8xMI355X" at 8 ranks,
+    every rank waiting for seven flags) ends with the oracle's one-process Q for that
+    set over the driver's 25 launches"""
     env = dict(os.environ, RLAMD_DIST_BACKEND="gloo", RLAMD_COLLECTIVE="peer")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
