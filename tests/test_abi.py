@@ -41,6 +41,32 @@ def test_library_exports_every_declared_symbol(rl):
     assert "gfx950" in info and "RLAMD_EXP=0" in info and "-ffp-contract=off" in info, info
 
 
+def test_header_is_plain_c_and_links(rl, tmp_path):
+    """The drop-in boundary is a C ABI: include/rl.h compiles as ISO C11 with
+    -pedantic -Werror (what cgo / bindgen / any FFI would parse), a C program that
+    takes the address of every declared function links against librlamd.so, and
+    its GPU-free calls answer (no compute: this container has no GPU)"""
+    names = declared_functions()
+    prog = tmp_path / "abi.c"
+    prog.write_text(
+        "#include <stdio.h>\n#include \"rl.h\"\n"
+        "typedef void (*fp)(void);\n"
+        "static const fp every[] = {\n" + ",\n".join(f"    (fp){n}" for n in names) + "\n};\n"
+        "int main(void) {\n"
+        "    printf(\"%d %u %s\\n\", rl_abi_version(), (unsigned)(sizeof every / sizeof every[0]), rl_build_id());\n"
+        "    return rl_abi_version() == RL_ABI_VERSION ? 0 : 1;\n}\n")
+    exe = tmp_path / "abi"
+    libdir = os.path.dirname(rl.LIB_PATH)
+    cc = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I",
+                         os.path.join(ROOT, "include"), str(prog), "-L", libdir, "-lrlamd",
+                         f"-Wl,-rpath,{libdir}", "-o", str(exe)], capture_output=True, text=True)
+    assert cc.returncode == 0, cc.stderr[-3000:]
+    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert run.returncode == 0, run.stderr
+    abi, n, bid = run.stdout.split()[:3]
+    assert int(abi) == 7 and int(n) == len(names) and bid.startswith("src:")
+
+
 def test_loaded_library_was_built_from_this_checkout(rl):
     """rl_build_id's source hash == the hash of the sources in this tree, so a stale
     librlamd.so (built from other sources) fails here instead of being benched or
