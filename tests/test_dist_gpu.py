@@ -43,6 +43,9 @@ CASES = {
     "taxi-ucb-esarsa": dict(env="taxi", selector="ucb", algo="expected_sarsa", group_size=512),
     "cliff-traces-sarsa": dict(env="cliff_walking", agent="traces", algo="sarsa", group_size=256),
     "blackjack-double-q": dict(env="blackjack", policy="double", algo="qlearning", group_size=512),
+    # UCB in the fixed point (cfg 8's regime): the fused peer merge also sums and
+    # applies the visit counts N and t
+    "taxi-ucb-qlearning": dict(env="taxi", selector="ucb", algo="qlearning", group_size=256),
 }
 
 
@@ -57,7 +60,8 @@ def test_two_rank_device_merge_equals_one_process(tmp_path, name):
     assert res["steps_ranks"] == res["steps_one"] > 0, res
     assert res["q_nonzero"] + res["q_nonfinite"] > 0, res   # UCB+E-SARSA: all-NaN/inf is legal (F7)
     assert res["q_equal"] and res["qf_equal"], res
-    assert res["q_repr"][0] == res["q_repr"][1] == ("fixed40" if name == "fl8x8-qlearning" else "f64"), res
+    assert res["q_repr"][0] == res["q_repr"][1] == (
+        "fixed40" if name in ("fl8x8-qlearning", "taxi-ucb-qlearning") else "f64"), res
     if "ucb_equal" in res:
         assert res["ucb_equal"], res
 
@@ -79,7 +83,8 @@ def test_two_rank_peer_merge_equals_one_process(tmp_path, name):
     assert res["steps_ranks"] == res["steps_one"] > 0, res
     assert res["q_nonzero"] + res["q_nonfinite"] > 0, res
     assert res["q_equal"] and res["qf_equal"], res
-    assert res["q_repr"][0] == res["q_repr"][1] == ("fixed40" if name == "fl8x8-qlearning" else "f64"), res
+    assert res["q_repr"][0] == res["q_repr"][1] == (
+        "fixed40" if name in ("fl8x8-qlearning", "taxi-ucb-qlearning") else "f64"), res
     if "ucb_equal" in res:
         assert res["ucb_equal"], res
 
