@@ -11,19 +11,28 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench")))[-1]
+# the latest round's bench lines: profiles/rNN_bench/ (rounds 1-5) or profiles/rNN/bench/ (6 on)
+ROUND = max(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench")) +
+            glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "bench")),
+            key=lambda d: int(os.path.relpath(d, os.path.join(ROOT, "profiles"))[1:3]))
+ROUND_NO = int(os.path.relpath(ROUND, os.path.join(ROOT, "profiles"))[1:3])
 LINES = sorted(glob.glob(os.path.join(ROUND, "*.json")))
+
+
+def bench_line(path):
+    """the bench's JSON line (a multi-rank run's file may also hold the launcher's chatter)"""
+    return json.loads([l for l in open(path).read().splitlines() if l.startswith("{")][-1])
 
 
 @pytest.mark.parametrize("path", LINES, ids=[os.path.basename(p) for p in LINES])
 def test_bench_line_roofline_is_consistent(path):
-    d = json.load(open(path))
+    d = bench_line(path)
     r = d["roofline"]
     assert 0.0 < r["frac"] <= 1.0, r["frac"]
     assert r["bound"] in ("latency", "valu", "hbm")
     # one step = the train launch + the merge: its kernel cannot take longer (bench
     # lines from round 5 on time the private rows' every launch)
-    if int(os.path.basename(ROUND)[1:3]) >= 5:
+    if ROUND_NO >= 5:
         assert 0.0 < r["kernel_avg_ms"] <= d["ms_per_step"], (r["kernel_avg_ms"], d["ms_per_step"])
     assert r["hbm"]["fused_frac"] <= 1.0
     if r["hbm"]["traffic_frac"] is not None:
@@ -42,7 +51,11 @@ def test_bench_line_roofline_is_consistent(path):
         assert r["bound"] == "hbm"
 
 
+def test_latest_round_is_checked():
+    assert ROUND_NO >= 6 and len(LINES) >= 12, (ROUND, len(LINES))
+
+
 def test_headline_line_is_the_default_workload():
-    d = json.load(open(os.path.join(ROUND, "bench_cfg2.json")))
+    d = bench_line(os.path.join(ROUND, "bench_cfg2.json"))
     assert d["config"]["survey_cfg"] == 2 and d["config"]["lanes_per_gpu"] == 1 << 20
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
